@@ -1,0 +1,228 @@
+"""bench.py — device-resident Mpps of the UPE worker hot path on MI355X (BASELINE.json metric).
+
+A "step" is one pass of the hot path (classify + finalize through the C ABI upe_gpu_process)
+over one batch already resident in HBM.  At N=1 the workload is BASELINE.json configs[1]
+(config B: 1M x 64 B UDP/IPv4, 8 rules).  Every step gets its own pristine copy of the batch
+(the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the work),
+which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU, each with its own static shard of the packet stream (a full config-B batch per step,
+tables replicated), no data-path collective — weak scaling.  torch.distributed carries only the
+barrier and the max-over-ranks time.
+
+Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per classify launch
+(B(p) = 8 + E(p) + 4 + W(p)) / the classify kernel's mean duration, measured
+with HIP events on the launch stream over the timed region.  cpu_baseline = the reference
+src/worker.c (oracle/_ref, built from the reference sources) timed on this host's cores over a
+bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
+WORKLOADS = {
+    "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",
+    "C": "C: 1M IMIX 64/570/1518 v4+v6, 1k 5-tuple rules, ARP+NDP L3 fwd (configs[2])",
+    "D": "D: 16M mixed/malformed, 64k rules (configs[3])",
+}
+
+
+def algorithmic_bytes(wl, verdict: np.ndarray) -> np.ndarray:
+    """B(p) per packet, SURVEY.md §8(d)."""
+    from upe_amd.layout import desc_lens, desc_offsets
+
+    offs = desc_offsets(wl.desc)
+    lens = desc_lens(wl.desc)
+    fr = wl.frames
+    et = (fr[offs + 12].astype(np.int64) << 8) | fr[offs + 13]
+    is4 = et == 0x0800
+    is6 = et == 0x86DD
+    ihl = (fr[offs + 14] & 0xF).astype(np.int64)
+    proto = np.where(is4, fr[offs + 23], np.where(is6, fr[offs + 20], 0)).astype(np.int64)
+    l3 = np.where(is4, ihl * 4, 40)
+    l4 = np.where(proto == 6, 20, 8)
+    code = verdict & 0xF
+    parsed = (code != 0) & (code != 5)
+    ext = np.where(parsed, 14 + l3 + l4, 34)
+    ext = np.where((code == 5) | (et == 0x0806), 78, ext)
+    E = np.minimum(lens, ext)
+    fwd = code == 4
+    hit = (verdict & 0x10) != 0
+    W = np.where(fwd & is4, 3, 0) + np.where(fwd & is6, 1, 0) + np.where(fwd & hit, 12, 0)
+    return 8 + E + 4 + W
+
+
+def cpu_baseline(wl, threads: int) -> dict:
+    import oracle
+
+    sample = f"{wl.n} packets of the same workload, median of 9 passes after 1 warm-up"
+    if oracle.ref_available():
+        cpus = sorted(os.sched_getaffinity(0))[:threads]
+        v1 = oracle.time_reference(wl, threads=1, cpus=cpus[:1], reps=9)
+        vn = oracle.time_reference(wl, threads=len(cpus), cpus=cpus, reps=9) if len(cpus) > 1 else v1
+        try:
+            model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                     if l.startswith("model name")][0]
+        except Exception:
+            model = "unknown"
+        return {"value": round(vn / 1e6, 3), "unit": "Mpps", "cores": len(cpus),
+                "kind": "reference", "single_core_value": round(v1 / 1e6, 3),
+                "cpu_model": model,
+                "sample": sample + "; reference src/worker.c process_packet + TX-flush loop "
+                          "(bursts of 32), one shard and calloc'd worker_t per pinned thread"}
+    # no reference build on this host: time the restatement, single core
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        oracle.run_restated(wl)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(wl.n / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+            "sample": sample}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="B", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=None, help="override batch size")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--max-copies", type=int, default=1024)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from upe_amd import gpu, synth
+
+    # this rank's static shard: a full batch of the configuration, its own seed
+    make = {"B": synth.config_b, "C": synth.config_c, "D": synth.config_d}[args.config]
+    kw = {"seed": {"B": 2, "C": 3, "D": 4}[args.config] + 1000 * rank}
+    if args.packets:
+        kw["n"] = args.packets
+    wl = make(**kw)
+    n = wl.n
+
+    worker = gpu.GpuWorker(local, wl.capacity)
+    worker.configure(wl)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    fbytes = int(wl.frames.nbytes)
+    stride = (fbytes + 255) // 256 * 256
+    copies = min(args.steps + args.warmup, args.max_copies)
+    pristine = torch.from_numpy(wl.frames).to(dev)
+    pool = torch.empty(copies * stride, dtype=torch.uint8, device=dev)
+    for c in range(copies):
+        pool[c * stride: c * stride + fbytes].copy_(pristine)
+    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    base = pool.data_ptr()
+    torch.cuda.synchronize(dev)
+
+    def step(k: int) -> None:
+        worker.process(base + (k % copies) * stride, desc, verdict, n, sh)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    v_first = verdict.cpu().numpy().view(np.uint32).copy()  # warm-up batch 0 verdicts
+
+    worker.timing_enable(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    classify_ms, finalize_ms, launches = worker.timing_read()
+    worker.timing_enable(False)
+
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([n * args.steps], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        total_packets = float(tot.item())
+    else:
+        total_packets = float(n * args.steps)
+
+    if rank == 0:
+        bpp = algorithmic_bytes(wl, v_first)
+        bytes_per_launch = float(bpp.sum())
+        kern_s = classify_ms / max(launches, 1) / 1e3
+        achieved = bytes_per_launch / kern_s / 1e9
+        ms_step = elapsed / args.steps * 1e3
+        out = {
+            "metric": METRIC,
+            "value": round(total_packets / elapsed / 1e6, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded upe_amd.synth, per-rank shard), resident in HBM",
+            "config": {"workload": WORKLOADS[args.config], "packets_per_gpu_step": n,
+                       "rules": int(len(wl.rules)), "parallelism": f"static shards x{world}, "
+                       "tables replicated, no RCCL on the data path"},
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "kernel": "upe_classify",
+                "kernel_ms": round(kern_s * 1e3, 5),
+                "finalize_ms": round(finalize_ms / max(launches, 1), 5),
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "algorithmic_bytes_per_packet": round(bytes_per_launch / n, 2),
+                "kernel_mpps": round(n / kern_s / 1e6, 1),
+            },
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    worker.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

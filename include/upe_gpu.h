@@ -1,0 +1,264 @@
+/*
+ * upe_gpu.h — C ABI of the MI355X batch dataplane for UPE's per-packet worker hot path.
+ *
+ * This is the drop-in boundary.  The reference runs the path one packet at a
+ * time inside process_packet() (reference src/worker.c:106-253): parse_flow_key()
+ * (src/parser.c:6-111) -> rule_table_match() (src/rule_table.c:163-176) -> counters and
+ * rule_stats (src/worker.c:119-153) -> L3 forward rewrite with the one-entry L1 neighbour caches
+ * and arp_get_mac()/ndp_get_mac() (src/worker.c:155-244, src/arp_table.c:55-80,
+ * src/ndp_table.c:67-86).  This library runs the same semantics over a whole batch of packets
+ * resident in GPU memory with one HIP kernel, bit-exact per packet.
+ *
+ * The reference surface is kept as plain data: every struct below is an ABI mirror of the
+ * reference layout (same size, same offsets, checked by _Static_assert), so a C caller passes
+ * rt->rules / arpt->entries / ndpt->entries / tx->eth_addr straight through without conversion.
+ *
+ * Conventions follow the reference (SURVEY.md §8(b) "Errors"): int 0 on success / -1 on failure,
+ * NULL for a failed constructor, and upe_gpu_last_error() for a message (thread-local).  No C++
+ * exception crosses this ABI.  A context is owned by one worker thread (one HIP stream); it is
+ * not internally locked, exactly like a reference worker_t.
+ */
+#ifndef UPE_GPU_H
+#define UPE_GPU_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* ABI mirrors of the reference layouts                                                        */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Mirrors ip_addr_t, reference include/parser.h:129-132.  IPv4 is host order in .v4 (ntohl),
+ * IPv6 is wire-order bytes. */
+typedef union {
+    uint32_t v4;
+    uint8_t v6[16];
+} upe_ip_addr_t;
+
+/* Mirrors flow_key_t, reference include/parser.h:134-141 (44 bytes). */
+typedef struct {
+    uint8_t ip_ver;
+    upe_ip_addr_t src_ip;
+    upe_ip_addr_t dst_ip;
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t protocol;
+} upe_flow_key_t;
+
+/* Mirrors action_type_t / flow_action_t, reference include/rule_table.h:9-17. */
+enum { UPE_ACT_DROP = 0, UPE_ACT_FWD = 1 };
+typedef struct {
+    int32_t type;        /* action_type_t is an int-sized enum */
+    int32_t out_ifindex; /* never read by the worker (all TX goes to tx->ifindex) */
+} upe_flow_action_t;
+
+/* Mirrors rule_t, reference include/rule_table.h:19-35 (92 bytes). */
+typedef struct {
+    uint32_t priority;
+    uint8_t ip_ver;
+    upe_ip_addr_t src_ip;
+    upe_ip_addr_t src_mask;
+    upe_ip_addr_t dst_ip;
+    upe_ip_addr_t dst_mask;
+    uint16_t src_port;
+    uint16_t dst_port;
+    uint8_t protocol;
+    upe_flow_action_t action;
+    uint32_t rule_id;
+} upe_rule_t;
+
+/* Mirrors arp_entry_t, reference include/arp_table.h:13-18 (32 bytes on LP64). */
+typedef struct {
+    uint32_t ip;
+    uint8_t mac[6];
+    int64_t update_at; /* time_t */
+    bool valid;
+} upe_arp_entry_t;
+
+/* Mirrors ndp_entry_t, reference include/ndp_table.h:13-18 (40 bytes on LP64). */
+typedef struct {
+    uint8_t ip[16];
+    uint8_t mac[6];
+    int64_t update_at; /* time_t */
+    bool valid;
+} upe_ndp_entry_t;
+
+/* Mirrors rule_stat_t, reference include/worker.h:18-21. */
+typedef struct {
+    uint64_t packets;
+    uint64_t bytes;
+} upe_rule_stat_t;
+
+/* The worker's one-entry neighbour caches, reference include/worker.h:56-63 (worker_t fields
+ * last_arp_ip / last_arp_mac / last_ndp_ip / last_ndp_mac).  A calloc'd worker starts all-zero. */
+typedef struct {
+    uint32_t last_arp_ip;
+    uint8_t last_arp_mac[6];
+    uint8_t last_ndp_ip[16];
+    uint8_t last_ndp_mac[6];
+} upe_l1_state_t;
+
+/* Per-worker counters, reference include/worker.h:37-41 plus the control-path tallies the
+ * reference does not keep separately.  pkts_forwarded counts FWD verdicts (queued for TX); with
+ * the reference's TX stub (tests/benchmark_throughput.c:37-42) that equals its forwarded count. */
+typedef struct {
+    uint64_t pkts_in;
+    uint64_t pkts_parsed;
+    uint64_t pkts_matched;
+    uint64_t pkts_forwarded;
+    uint64_t pkts_dropped;
+    uint64_t pkts_consumed; /* NDP NS/NA eaten by handle_control_packet (src/worker.c:96-98) */
+    uint64_t arp_learn;     /* ARP packets that reach arp_update (src/worker.c:31-35) */
+    uint64_t arp_reply;     /* ARP requests answered in place (src/worker.c:40-52) */
+} upe_counters_t;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Per-packet verdict word                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+/* bits 0-3  : verdict code (which exit of process_packet the packet took)
+ * bits 4-7  : flags
+ * bits 8-31 : index of the matched rule in the caller's sorted rules[] array, plus one
+ *             (0 = no rule matched).  rules[idx].rule_id indexes rule_stats. */
+enum {
+    UPE_V_DROP_PARSE = 0,   /* parse_flow_key failed   src/worker.c:117-125 */
+    UPE_V_DROP_NOMATCH = 1, /* no rule                 src/worker.c:130-137 */
+    UPE_V_DROP_RULE = 2,    /* ACT_DROP                src/worker.c:146-153 */
+    UPE_V_DROP_TTL = 3,     /* TTL / hop limit <= 1    src/worker.c:165-172, 204-211 */
+    UPE_V_FWD = 4,          /* queued for TX           src/worker.c:155-244 */
+    UPE_V_CONSUMED = 5,     /* NDP NS/NA consumed      src/worker.c:57-100 */
+    UPE_V_DROP_ACTION = 6   /* unknown action type     src/worker.c:247-252 */
+};
+enum {
+    UPE_VF_NEIGH_HIT = 0x10, /* MACs rewritten: dst = neighbour MAC, src = port MAC */
+    UPE_VF_ARP_LEARN = 0x20, /* well-formed ARP: caller must arp_update(spa, sha) */
+    UPE_VF_ARP_REPLY = 0x40, /* ARP request for our IPv4: frame rewritten in place into the
+                                reply; caller must tx_send it */
+    UPE_VF_L1_INIT = 0x80    /* forwarded v4/v6 packet whose destination equals the L1 cache
+                                address the batch started with (ARP: and that address != 0) */
+};
+#define UPE_VERDICT_CODE(v) ((v) & 0xFu)
+#define UPE_VERDICT_RULE(v) ((int64_t)((v) >> 8) - 1)
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batch layout in GPU memory                                                                  */
+/* ------------------------------------------------------------------------------------------ */
+/* frames : one device buffer holding the frames back to back.  Every frame starts on a 16-byte
+ *          boundary, and at least UPE_FRAME_TAIL readable bytes must follow each frame start
+ *          (pad the buffer end).  Bytes at or beyond a frame's length are never used.
+ * desc[i]: (byte_offset << 16) | len, len <= 65535.  A frame may be a header window shorter
+ *          than len as long as it holds the first min(len, UPE_HDR_WINDOW) bytes.
+ * verdict: n uint32 words, written by the kernel.
+ * A batch is one constant-table segment: control packets (ARP, NDP NS/NA) in it are classified
+ * exactly, but their table updates are applied by the caller after the batch (split batches at
+ * control packets for exact sequential semantics). */
+#define UPE_HDR_WINDOW 96
+#define UPE_FRAME_TAIL 96
+#define UPE_DESC(off, len) ((((uint64_t)(off)) << 16) | ((uint64_t)(len) & 0xFFFFu))
+
+/* Result summary of the last processed batch. */
+typedef struct {
+    upe_counters_t counters; /* this batch only */
+    uint64_t n_ctrl;         /* control packets (ARP + NDP NS/NA) in the batch */
+    uint64_t first_ctrl;     /* index of the first one, or UINT64_MAX */
+} upe_batch_info_t;
+
+typedef struct upe_gpu_ctx upe_gpu_ctx_t;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Entry points                                                                                */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Last error message of the calling thread ("" if none). */
+const char *upe_gpu_last_error(void);
+
+/* Number of visible GPUs, or -1. */
+int upe_gpu_device_count(void);
+
+/* Open a context on `device`, with its own HIP stream.  Replaces the per-worker state set up by
+ * worker_init() (reference src/worker.c:309-330): counters, rule_stats sized by
+ * rule_capacity (= rt->capacity, src/worker.c:326), calloc'd L1 caches. */
+upe_gpu_ctx_t *upe_gpu_open(int device, size_t rule_capacity);
+void upe_gpu_close(upe_gpu_ctx_t *ctx);
+
+/* Upload the rule table: rules[0..count) in the order rule_table_t keeps them (sorted by
+ * (priority, rule_id), reference src/rule_table.c:96-109,158).  Replaces the read-only borrow of
+ * w->rt (src/worker.c:129).  count <= rule capacity given at open, every rule_id < capacity. */
+int upe_gpu_load_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count);
+
+/* Upload a snapshot of the neighbour tables' slot arrays (arpt->entries / ndpt->entries with
+ * their power-of-two capacities).  Lookups probe exactly as arp_get_mac/ndp_get_mac do.
+ * Either table may be NULL with capacity 0 (every lookup misses). */
+int upe_gpu_load_neigh(upe_gpu_ctx_t *ctx, const upe_arp_entry_t *arp, size_t arp_capacity,
+                       const upe_ndp_entry_t *ndp, size_t ndp_capacity);
+
+/* The TX port identity the worker reads from tx_ctx_t (include/tx.h:9-14): own MAC (source MAC of
+ * forwarded frames, src/worker.c:199,229) and own IPv4 (ARP replies, src/worker.c:40). */
+int upe_gpu_set_port(upe_gpu_ctx_t *ctx, const uint8_t eth_addr[6], uint32_t ip4_addr);
+
+/* L1 neighbour-cache state (kept on the device between batches). */
+int upe_gpu_set_l1(upe_gpu_ctx_t *ctx, const upe_l1_state_t *l1);
+int upe_gpu_get_l1(upe_gpu_ctx_t *ctx, upe_l1_state_t *l1);
+
+/* Process one batch resident in GPU memory (see "Batch layout").  Asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's own stream).  Frames are rewritten in place exactly as
+ * process_packet rewrites b->data.  Counters, rule stats and the L1 state accumulate in the
+ * context, as they do in worker_t. */
+int upe_gpu_process(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                    uint32_t *d_verdict, size_t n, void *stream);
+
+/* Wait for all work queued on the context's stream (or `stream`). */
+int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
+
+/* Summary of the most recent upe_gpu_process() (synchronises). */
+int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
+
+/* Accumulated worker counters and rule_stats[0..capacity) (synchronises). */
+int upe_gpu_get_stats(upe_gpu_ctx_t *ctx, upe_counters_t *counters, upe_rule_stat_t *rule_stats,
+                      size_t capacity);
+int upe_gpu_reset_stats(upe_gpu_ctx_t *ctx);
+
+/* Kernel timing.  While enabled, every upe_gpu_process() records HIP events on its stream
+ * around the classify kernel and the finalize kernel.  upe_gpu_timing_read() synchronises and
+ * returns the summed durations (ms) and the number of process() calls since enabling. */
+int upe_gpu_timing_enable(upe_gpu_ctx_t *ctx, int enable);
+int upe_gpu_timing_read(upe_gpu_ctx_t *ctx, double *classify_ms, double *finalize_ms,
+                        uint64_t *launches);
+
+/* Device memory helpers so a C caller needs no HIP headers. */
+void *upe_gpu_malloc(upe_gpu_ctx_t *ctx, size_t bytes);
+int upe_gpu_free(upe_gpu_ctx_t *ctx, void *dptr);
+int upe_gpu_memcpy_h2d(upe_gpu_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int upe_gpu_memcpy_d2h(upe_gpu_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+/* Layout checks against the reference (LP64). */
+#ifdef __cplusplus
+#define UPE_STATIC_ASSERT static_assert
+#else
+#define UPE_STATIC_ASSERT _Static_assert
+#endif
+UPE_STATIC_ASSERT(sizeof(upe_flow_key_t) == 44, "flow_key_t layout");
+UPE_STATIC_ASSERT(offsetof(upe_flow_key_t, dst_ip) == 20, "flow_key_t.dst_ip");
+UPE_STATIC_ASSERT(offsetof(upe_flow_key_t, protocol) == 40, "flow_key_t.protocol");
+UPE_STATIC_ASSERT(sizeof(upe_rule_t) == 92, "rule_t layout");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, src_ip) == 8, "rule_t.src_ip");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, dst_mask) == 56, "rule_t.dst_mask");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, src_port) == 72, "rule_t.src_port");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, protocol) == 76, "rule_t.protocol");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, action) == 80, "rule_t.action");
+UPE_STATIC_ASSERT(offsetof(upe_rule_t, rule_id) == 88, "rule_t.rule_id");
+UPE_STATIC_ASSERT(sizeof(upe_arp_entry_t) == 32, "arp_entry_t layout");
+UPE_STATIC_ASSERT(offsetof(upe_arp_entry_t, valid) == 24, "arp_entry_t.valid");
+UPE_STATIC_ASSERT(sizeof(upe_ndp_entry_t) == 40, "ndp_entry_t layout");
+UPE_STATIC_ASSERT(offsetof(upe_ndp_entry_t, valid) == 32, "ndp_entry_t.valid");
+UPE_STATIC_ASSERT(sizeof(upe_rule_stat_t) == 16, "rule_stat_t layout");
+
+#endif /* UPE_GPU_H */

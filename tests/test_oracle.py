@@ -1,0 +1,245 @@
+"""The oracle pinned before it is trusted (CPU only):
+
+* known-answer tests of reference tests/test_suite.c restated against our C restatement
+  (test_tcp_packet_parser :132-165, test_icmp_packet_parser :168-199, test_ipv6_packet_parser
+  :202-242, test_flow_hash :245-299, test_ipv4_checksum_and_ttl :332-362, test_arp_table /
+  test_ndp_table :365-437, test_ipv6_rule_matching :523-590, test_rule_priority :107-129);
+* every golden vector in tests/golden/ (outputs of the reference worker itself);
+* the reference harness itself where it is built (oracle/_ref), on fresh seeds.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+import golden_io
+import oracle
+from upe_amd import synth
+from upe_amd.layout import ARP_DTYPE, NDP_DTYPE, RULE_DTYPE
+
+lib = oracle.oracle_lib()
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def parse(buf: bytes, ln: int):
+    rc, key = oracle.parse(buf, ln)
+    k = key
+    out = {"ver": int(k[0]), "src4": int.from_bytes(bytes(k[4:8]), "little"),
+           "dst4": int.from_bytes(bytes(k[20:24]), "little"), "src6": bytes(k[4:20]),
+           "dst6": bytes(k[20:36]), "sport": int.from_bytes(bytes(k[36:38]), "little"),
+           "dport": int.from_bytes(bytes(k[38:40]), "little"), "proto": int(k[40])}
+    return rc, out
+
+
+# ---- tests/test_suite.c:132-165 ----
+def test_tcp_parser_gates():
+    pkt = bytearray(128)
+    assert parse(bytes(pkt), 12)[0] == -1
+    pkt[12:14] = b"\x08\x00"
+    assert parse(bytes(pkt), 17)[0] == -1
+    pkt[14] = 0x45
+    pkt[14 + 9] = 6
+    assert parse(bytes(pkt), 37)[0] == -1
+    pkt[14 + 20 + 12] = 0x50
+    assert parse(bytes(pkt), 60)[0] == 0
+
+
+# ---- tests/test_suite.c:168-199 ----
+def test_icmp_parser_kat():
+    pkt = bytearray(128)
+    pkt[12:14] = b"\x08\x00"
+    pkt[14] = 0x45
+    pkt[23] = 1
+    pkt[34] = 8
+    pkt[35] = 0
+    pkt[38:40] = (0x1234).to_bytes(2, "big")
+    rc, k = parse(bytes(pkt), 42)
+    assert rc == 0 and k["proto"] == 1 and k["sport"] == 0x1234 and k["dport"] == 0x0800
+    assert parse(bytes(pkt), 38)[0] == -1
+
+
+# ---- tests/test_suite.c:202-242 ----
+def test_ipv6_parser_kat():
+    src = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [1])
+    dst = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [2])
+    pkt = bytearray(128)
+    pkt[12:14] = b"\x86\xdd"
+    pkt[14:18] = (0x60000000).to_bytes(4, "big")
+    pkt[18:20] = (20).to_bytes(2, "big")
+    pkt[20] = 6
+    pkt[21] = 64
+    pkt[22:38] = src
+    pkt[38:54] = dst
+    pkt[54:56] = (46500).to_bytes(2, "big")
+    pkt[56:58] = (443).to_bytes(2, "big")
+    pkt[66] = 0x50
+    rc, k = parse(bytes(pkt), 74)
+    assert rc == 0 and k["ver"] == 6 and k["proto"] == 6
+    assert k["src6"] == src and k["dst6"] == dst
+
+
+# ---- tests/test_suite.c:245-299 ----
+def _key(ver, s, d, sp, dp, proto):
+    k = np.zeros(44, np.uint8)
+    k[0] = ver
+    if ver == 4:
+        k[4:8] = np.frombuffer(s.to_bytes(4, "little"), np.uint8)
+        k[20:24] = np.frombuffer(d.to_bytes(4, "little"), np.uint8)
+    else:
+        k[4:20] = np.frombuffer(s, np.uint8)
+        k[20:36] = np.frombuffer(d, np.uint8)
+    k[36:38] = np.frombuffer(sp.to_bytes(2, "little"), np.uint8)
+    k[38:40] = np.frombuffer(dp.to_bytes(2, "little"), np.uint8)
+    k[40] = proto
+    return k
+
+
+def test_flow_hash_symmetry():
+    h = lambda k: lib.upe_ref_flow_hash(_p(k))  # noqa: E731
+    k1 = _key(4, 0x0A800001, 0x0A800002, 12121, 443, 6)
+    k2 = _key(4, 0x0A800002, 0x0A800001, 443, 12121, 6)
+    k3 = _key(4, 0x0A800003, 0x0A800002, 12121, 443, 6)
+    assert h(k1) == h(k1) == h(k2) and h(k1) != h(k3)
+    a1 = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [1])
+    a2 = bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [2])
+    assert h(_key(6, a1, a2, 12121, 443, 6)) == h(_key(6, a2, a1, 443, 12121, 6))
+
+
+# ---- tests/test_suite.c:332-362 ----
+def test_checksum_and_ttl_kat():
+    ip = np.array([0x45, 0, 0, 0x14, 0, 0, 0, 0, 0x40, 6, 0, 0, 10, 0, 0, 1, 10, 0, 0, 2],
+                  np.uint8)
+    cs = lib.upe_ref_ipv4_checksum(_p(ip), 20)
+    ip[10], ip[11] = cs & 0xFF, cs >> 8
+    assert lib.upe_ref_ipv4_checksum(_p(ip), 20) == 0
+    ip[8] -= 1
+    ip[10] = ip[11] = 0
+    cs2 = lib.upe_ref_ipv4_checksum(_p(ip), 20)
+    ip[10], ip[11] = cs2 & 0xFF, cs2 >> 8
+    assert ip[8] == 63 and lib.upe_ref_ipv4_checksum(_p(ip), 20) == 0 and cs != cs2
+
+
+# ---- tests/test_suite.c:523-590 (+ ipv4 helper, src/rule_table.c:14-30) ----
+def test_mask_helpers():
+    m = np.zeros(16, np.uint8)
+    assert lib.upe_ref_ipv6_mask(0, _p(m)) and not m.any()
+    assert lib.upe_ref_ipv6_mask(128, _p(m)) and (m == 0xFF).all()
+    assert not lib.upe_ref_ipv6_mask(129, _p(m))
+    assert lib.upe_ref_ipv6_mask(1, _p(m)) and m[0] == 0x80 and m[1] == 0
+    for p in range(0, 129):
+        assert lib.upe_ref_ipv6_mask(p, _p(m))
+        assert bytes(m) == synth.ipv6_mask(p)
+    v = np.zeros(1, np.uint32)
+    for p in range(0, 33):
+        assert lib.upe_ref_ipv4_mask(p, _p(v)) and int(v[0]) == synth.ipv4_mask(p)
+    assert not lib.upe_ref_ipv4_mask(33, _p(v))
+    assert synth.ipv4_mask(17) == 0xFFFF8000
+
+
+def test_ipv6_rule_matching_kat():
+    rules = synth.rules_array([
+        synth.make_rule(100, 1, ip_ver=6, src=(bytes.fromhex("20010db8") + bytes(12), 32)),
+        synth.make_rule(99999, 0),
+    ])
+    rt = synth.build_rule_table(rules)
+    k1 = _key(6, bytes.fromhex("20010db8") + bytes(11) + b"\x01", bytes(16), 0, 0, 6)
+    k2 = _key(6, bytes.fromhex("20800db8") + bytes(11) + b"\x01", bytes(16), 0, 0, 6)
+    assert rt[lib.upe_ref_match(_p(rt), len(rt), _p(k1))]["action"] == 1
+    assert rt[lib.upe_ref_match(_p(rt), len(rt), _p(k2))]["action"] == 0
+
+
+# ---- tests/test_suite.c:107-129 ----
+def test_rule_priority_sort():
+    rules = synth.rules_array([synth.make_rule(100, 0), synth.make_rule(10, 0),
+                               synth.make_rule(66, 0)])
+    rt = synth.build_rule_table(rules)
+    assert rt["priority"].tolist() == [10, 66, 100]
+    out = np.zeros(3, RULE_DTYPE)
+    lib.upe_ref_rules_build(_p(rules), 3, _p(out))
+    assert out["priority"].tolist() == [10, 66, 100]
+    assert out["rule_id"].tolist() == [1, 2, 0]
+
+
+# ---- tests/test_suite.c:365-437 ----
+def test_neighbour_tables():
+    t = synth.arp_table(16, [(0x0A800001, bytes.fromhex("aabb11223344"))])
+    mac = np.zeros(6, np.uint8)
+    assert lib.upe_ref_arp_lookup(_p(t), 16, 0x0A800001, _p(mac))
+    assert bytes(mac) == bytes.fromhex("aabb11223344")
+    assert not lib.upe_ref_arp_lookup(_p(t), 16, 0x0AAA015C, _p(mac))
+    t = synth.arp_table(16, [(0x0A800001, bytes.fromhex("aabb11223344")),
+                             (0x0A800001, bytes.fromhex("ccccbbbbaaaa"))])
+    assert lib.upe_ref_arp_lookup(_p(t), 16, 0x0A800001, _p(mac))
+    assert bytes(mac) == bytes.fromhex("ccccbbbbaaaa")
+    ip1 = bytes([0xD9, 0xCE, 0xA8, 0x81] + [0] * 8 + [0xBB, 0x12, 0, 0])
+    n = synth.ndp_table(16, [(ip1, bytes.fromhex("cc11aa4498ab"))])
+    ipa = np.frombuffer(ip1, np.uint8).copy()
+    assert lib.upe_ref_ndp_lookup(_p(n), 16, _p(ipa), _p(mac))
+    assert bytes(mac) == bytes.fromhex("cc11aa4498ab")
+    ip2 = np.frombuffer(bytes([0x19, 0x2A, 0x0D, 0xB2] + [0] * 11 + [1]), np.uint8).copy()
+    assert not lib.upe_ref_ndp_lookup(_p(n), 16, _p(ip2), _p(mac))
+
+
+# ---- the golden vectors produced by the reference worker ----
+@pytest.mark.parametrize("case", golden_io.CASES)
+def test_restated_oracle_matches_golden(case):
+    wl, ref = golden_io.load(case)
+    r = oracle.run_restated(wl, apply_control=True)
+    assert np.array_equal(r.verdict, ref["verdict"])
+    assert np.array_equal(r.frames, ref["frames"])
+    assert r.counters.tobytes() == ref["counters"].tobytes()
+    assert np.array_equal(r.rule_stats, ref["rule_stats"])
+    assert r.l1.tobytes() == ref["l1"].tobytes()
+    keep = ["ip", "mac", "valid"]
+    assert np.array_equal(r.arp[keep], ref["arp"][keep])
+    assert np.array_equal(r.ndp[keep], ref["ndp"][keep])
+
+
+@pytest.mark.parametrize("case", golden_io.CASES)
+def test_rule_table_build_matches_reference(case):
+    """synth.build_rule_table (used by bench and tests) == rt->rules after rule_table_add."""
+    wl, ref = golden_io.load(case)
+    got = wl.rules_sorted
+    for f in RULE_DTYPE.names:
+        assert np.array_equal(got[f], ref["rules_sorted"][f]), f
+
+
+def _sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("key,make", [("B_1M", synth.config_b), ("C_1M", synth.config_c)])
+def test_restated_oracle_matches_full_size_digest(key, make):
+    dg = golden_io.digests()[key]
+    wl = make()
+    assert _sha(wl.frames, wl.desc, wl.rules, wl.arp, wl.ndp) == dg["inputs"]
+    r = oracle.run_restated(wl)
+    assert _sha(r.verdict) == dg["verdict"]
+    assert _sha(r.frames) == dg["frames"]
+    assert _sha(r.rule_stats) == dg["rule_stats"]
+    assert _sha(r.l1) == dg["l1"]
+    assert [int(x) for x in r.counters[0].tolist()] == dg["counters"]
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference harness not built here")
+@pytest.mark.parametrize("seed", [21, 22])
+def test_restated_vs_reference_fresh_seeds(seed):
+    for make in (lambda: synth.config_c(n=6000, seed=seed),
+                 lambda: synth.config_d(n=3000, seed=seed, n_rules=512)):
+        wl = make()
+        a = oracle.run_restated(wl, apply_control=True)
+        b = oracle.run_reference(wl)
+        assert np.array_equal(a.verdict, b.verdict)
+        assert np.array_equal(a.frames, b.frames)
+        assert a.counters.tobytes() == b.counters.tobytes()
+        assert np.array_equal(a.rule_stats, b.rule_stats)
+        assert a.l1.tobytes() == b.l1.tobytes()

@@ -1,0 +1,265 @@
+"""ctypes binding of libupe_gpu.so (the C ABI of include/upe_gpu.h).
+
+This is host plumbing above the C ABI, mirroring the reference worker's interface: a
+`GpuWorker` plays the role of one worker_t (reference include/worker.h:23-69) — it owns the
+counters, rule_stats and L1 neighbour caches, borrows a rule table and neighbour-table snapshots,
+and processes batches.  Device buffers may be torch tensors (data_ptr) or raw device pointers;
+streams are hipStream_t handles (torch.cuda.current_stream().cuda_stream).
+
+There is no CPU fallback: if libupe_gpu.so is missing or fails to load, importing this module
+raises.  Build it with `make -C upe_amd/csrc` (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, L1_DTYPE, NDP_DTYPE,
+                     RULE_DTYPE, RULE_STAT_DTYPE)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")
+
+
+class UpeGpuError(RuntimeError):
+    pass
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built; run `make -C upe_amd/csrc` "
+                          "(the MI355X path has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    sig = {
+        "upe_gpu_last_error": (ctypes.c_char_p, []),
+        "upe_gpu_device_count": (I, []),
+        "upe_gpu_open": (P, [I, SZ]),
+        "upe_gpu_close": (None, [P]),
+        "upe_gpu_load_rules": (I, [P, P, SZ]),
+        "upe_gpu_load_neigh": (I, [P, P, SZ, P, SZ]),
+        "upe_gpu_set_port": (I, [P, P, ctypes.c_uint32]),
+        "upe_gpu_set_l1": (I, [P, P]),
+        "upe_gpu_get_l1": (I, [P, P]),
+        "upe_gpu_process": (I, [P, P, P, P, SZ, P]),
+        "upe_gpu_sync": (I, [P, P]),
+        "upe_gpu_batch_info": (I, [P, P]),
+        "upe_gpu_get_stats": (I, [P, P, P, SZ]),
+        "upe_gpu_reset_stats": (I, [P]),
+        "upe_gpu_timing_enable": (I, [P, I]),
+        "upe_gpu_timing_read": (I, [P, P, P, P]),
+        "upe_gpu_malloc": (P, [P, SZ]),
+        "upe_gpu_free": (I, [P, P]),
+        "upe_gpu_memcpy_h2d": (I, [P, P, P, SZ, P]),
+        "upe_gpu_memcpy_d2h": (I, [P, P, P, SZ, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+# every symbol include/upe_gpu.h declares (checked by tests/test_abi.py)
+EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_gpu_close",
+            "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_set_port", "upe_gpu_set_l1",
+            "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
+            "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
+            "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
+            "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise UpeGpuError(f"{what}: {LIB.upe_gpu_last_error().decode()}")
+
+
+def _np_ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dev_ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    return int(x.data_ptr())  # torch tensor
+
+
+def device_count() -> int:
+    return LIB.upe_gpu_device_count()
+
+
+class GpuWorker:
+    """One GPU-backed worker context (include/upe_gpu.h upe_gpu_ctx_t)."""
+
+    def __init__(self, device: int = 0, rule_capacity: int = 1024):
+        self._ctx = LIB.upe_gpu_open(device, rule_capacity)
+        if not self._ctx:
+            raise UpeGpuError(f"upe_gpu_open: {LIB.upe_gpu_last_error().decode()}")
+        self.device = device
+        self.capacity = rule_capacity
+
+    # ---- lifetime ----
+    def close(self) -> None:
+        if self._ctx:
+            LIB.upe_gpu_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- tables and identity ----
+    def load_rules(self, rules_sorted: np.ndarray) -> None:
+        r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
+        _check(LIB.upe_gpu_load_rules(self._ctx, _np_ptr(r) if len(r) else None, len(r)),
+               "upe_gpu_load_rules")
+
+    def load_neigh(self, arp: np.ndarray | None, ndp: np.ndarray | None) -> None:
+        a = np.ascontiguousarray(arp if arp is not None else np.zeros(0, ARP_DTYPE), ARP_DTYPE)
+        b = np.ascontiguousarray(ndp if ndp is not None else np.zeros(0, NDP_DTYPE), NDP_DTYPE)
+        _check(LIB.upe_gpu_load_neigh(self._ctx, _np_ptr(a) if len(a) else None, len(a),
+                                      _np_ptr(b) if len(b) else None, len(b)),
+               "upe_gpu_load_neigh")
+
+    def set_port(self, eth_addr: bytes, ip4_addr: int) -> None:
+        mac = np.frombuffer(bytes(eth_addr), np.uint8).copy()
+        _check(LIB.upe_gpu_set_port(self._ctx, _np_ptr(mac), ip4_addr), "upe_gpu_set_port")
+
+    def set_l1(self, l1: np.ndarray) -> None:
+        x = np.ascontiguousarray(l1, L1_DTYPE).reshape(1)
+        _check(LIB.upe_gpu_set_l1(self._ctx, _np_ptr(x)), "upe_gpu_set_l1")
+
+    def get_l1(self) -> np.ndarray:
+        x = np.zeros(1, L1_DTYPE)
+        _check(LIB.upe_gpu_get_l1(self._ctx, _np_ptr(x)), "upe_gpu_get_l1")
+        return x
+
+    def configure(self, wl) -> None:
+        """Load a synth.Workload's tables, port identity and starting L1 state."""
+        self.load_rules(wl.rules_sorted)
+        self.load_neigh(wl.arp, wl.ndp)
+        self.set_port(wl.eth_addr, wl.ip4_addr)
+        self.set_l1(wl.l1)
+
+    # ---- the hot path ----
+    def process(self, frames, desc, verdict, n: int, stream=None) -> None:
+        """Queue one batch (device buffers) on `stream` (hipStream_t handle or None)."""
+        _check(LIB.upe_gpu_process(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
+                                   _dev_ptr(verdict), n, stream or None),
+               "upe_gpu_process")
+
+    def sync(self, stream=None) -> None:
+        _check(LIB.upe_gpu_sync(self._ctx, stream or None), "upe_gpu_sync")
+
+    def batch_info(self) -> np.ndarray:
+        x = np.zeros(1, BATCH_INFO_DTYPE)
+        _check(LIB.upe_gpu_batch_info(self._ctx, _np_ptr(x)), "upe_gpu_batch_info")
+        return x
+
+    def get_stats(self):
+        c = np.zeros(1, COUNTERS_DTYPE)
+        s = np.zeros(self.capacity, RULE_STAT_DTYPE)
+        _check(LIB.upe_gpu_get_stats(self._ctx, _np_ptr(c), _np_ptr(s), self.capacity),
+               "upe_gpu_get_stats")
+        return c, s
+
+    def reset_stats(self) -> None:
+        _check(LIB.upe_gpu_reset_stats(self._ctx), "upe_gpu_reset_stats")
+
+    # ---- kernel timing (HIP events on the launch stream) ----
+    def timing_enable(self, on: bool = True) -> None:
+        _check(LIB.upe_gpu_timing_enable(self._ctx, int(on)), "upe_gpu_timing_enable")
+
+    def timing_read(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_uint64()
+        _check(LIB.upe_gpu_timing_read(self._ctx, ctypes.byref(a), ctypes.byref(b),
+                                       ctypes.byref(n)), "upe_gpu_timing_read")
+        return a.value, b.value, n.value
+
+    # ---- device memory without torch ----
+    def malloc(self, nbytes: int) -> int:
+        p = LIB.upe_gpu_malloc(self._ctx, nbytes)
+        if not p:
+            raise UpeGpuError(f"upe_gpu_malloc: {LIB.upe_gpu_last_error().decode()}")
+        return p
+
+    def free(self, ptr: int) -> None:
+        _check(LIB.upe_gpu_free(self._ctx, ptr), "upe_gpu_free")
+
+    def h2d(self, dptr: int, host: np.ndarray, stream=None) -> None:
+        _check(LIB.upe_gpu_memcpy_h2d(self._ctx, dptr, _np_ptr(host), host.nbytes, stream or None),
+               "upe_gpu_memcpy_h2d")
+
+    def d2h(self, host: np.ndarray, dptr: int, stream=None) -> None:
+        _check(LIB.upe_gpu_memcpy_d2h(self._ctx, _np_ptr(host), dptr, host.nbytes, stream or None),
+               "upe_gpu_memcpy_d2h")
+
+
+class DeviceBatch:
+    """A workload's batch copied into device memory owned by a GpuWorker."""
+
+    def __init__(self, worker: GpuWorker, frames: np.ndarray, desc: np.ndarray):
+        self.worker = worker
+        self.n = int(desc.shape[0])
+        self.frames_nbytes = int(frames.nbytes)
+        self.frames = worker.malloc(frames.nbytes)
+        self.desc = worker.malloc(max(desc.nbytes, 8))
+        self.verdict = worker.malloc(max(4 * self.n, 4))
+        worker.h2d(self.frames, np.ascontiguousarray(frames))
+        if self.n:
+            worker.h2d(self.desc, np.ascontiguousarray(desc))
+        worker.sync()
+
+    def run(self, stream=None) -> None:
+        self.worker.process(self.frames, self.desc, self.verdict, self.n, stream)
+
+    def fetch(self):
+        """(frames, verdict) back to the host (synchronises)."""
+        self.worker.sync()
+        frames = np.empty(self.frames_nbytes, np.uint8)
+        verdict = np.empty(self.n, np.uint32)
+        self.worker.d2h(frames, self.frames)
+        if self.n:
+            self.worker.d2h(verdict, self.verdict)
+        self.worker.sync()
+        return frames, verdict
+
+    def free(self) -> None:
+        for p in (self.frames, self.desc, self.verdict):
+            self.worker.free(p)
+        self.frames = self.desc = self.verdict = 0
+
+
+def run_workload(wl, device: int = 0, worker: GpuWorker | None = None):
+    """Process a synth.Workload once on the GPU; returns (frames, verdict, counters,
+    rule_stats, l1) like oracle.Result."""
+    own = worker is None
+    w = worker or GpuWorker(device, wl.capacity)
+    try:
+        if own:
+            w.configure(wl)
+        b = DeviceBatch(w, wl.frames, wl.desc)
+        b.run()
+        frames, verdict = b.fetch()
+        b.free()
+        counters, stats = w.get_stats()
+        l1 = w.get_l1()
+        return frames, verdict, counters, stats, l1
+    finally:
+        if own:
+            w.close()

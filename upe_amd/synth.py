@@ -1,0 +1,781 @@
+"""Seeded synthetic workloads for the BASELINE.json configurations.
+
+Everything here is deterministic given the seed (numpy PCG64), so the GPU box regenerates
+byte-identical batches and the committed golden digests stay valid.  Frames are built in wire
+order into a 2-D header matrix and then packed into the batch layout of include/upe_gpu.h
+(16-byte aligned starts, uint64 descriptors, FRAME_TAIL bytes of tail padding).
+
+Config names follow BASELINE.json "configs":
+  A  10k x 64 B Eth/IPv4/UDP, rules.example (reference rules.example:3-25), CPU replay
+  B  1M x 64 B IPv4/UDP, 8 rules (every field type), ARP 240/256 hit
+  C  IMIX 64/570/1518 (7:4:1), 70 % IPv4 / 30 % IPv6, 1k 5-tuple rules, ARP+NDP ~600 each
+  D  16M packets, 64k rules, IHL/doff 5-15, 10 % malformed, v4/v6 interleaved
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from .layout import (ACT_DROP, ACT_FWD, ARP_DTYPE, FRAME_TAIL, NDP_DTYPE, RULE_DTYPE,
+                     l1_zero, make_desc)
+
+PORT_MAC = bytes([0x02, 0x00, 0x00, 0x00, 0x00, 0x01])
+PORT_IP4 = 0x0A8000FE  # 10.128.0.254
+
+
+@dataclasses.dataclass
+class Workload:
+    name: str
+    frames: np.ndarray        # uint8, packed batch + FRAME_TAIL padding
+    desc: np.ndarray          # uint64 (offset << 16 | len)
+    rules: np.ndarray         # RULE_DTYPE in insertion order (what rule_table_add receives)
+    capacity: int             # rule table capacity (rule_stats size)
+    arp: np.ndarray           # ARP_DTYPE slot array (power-of-two length)
+    ndp: np.ndarray           # NDP_DTYPE slot array
+    eth_addr: bytes = PORT_MAC
+    ip4_addr: int = PORT_IP4
+    l1: np.ndarray = dataclasses.field(default_factory=l1_zero)
+
+    @property
+    def n(self) -> int:
+        return int(self.desc.shape[0])
+
+    @property
+    def rules_sorted(self) -> np.ndarray:
+        return build_rule_table(self.rules)
+
+    def copy(self) -> "Workload":
+        return dataclasses.replace(self, frames=self.frames.copy(), desc=self.desc.copy(),
+                                   arp=self.arp.copy(), ndp=self.ndp.copy(), l1=self.l1.copy())
+
+
+# ---------------------------------------------------------------------------------------------
+# rule table: rule_table_add semantics (reference src/rule_table.c:130-161), one sort at the end
+# ---------------------------------------------------------------------------------------------
+
+def ipv4_mask(prefix: int) -> int:
+    """ipv4_mask_from_prefix, reference src/rule_table.c:14-30 (host-order value)."""
+    if not 0 <= prefix <= 32:
+        raise ValueError("prefix > 32")
+    return 0 if prefix == 0 else (0xFFFFFFFF << (32 - prefix)) & 0xFFFFFFFF
+
+
+def ipv6_mask(prefix: int) -> bytes:
+    """ipv6_mask_from_prefix, reference src/rule_table.c:32-50."""
+    if not 0 <= prefix <= 128:
+        raise ValueError("prefix > 128")
+    out = bytearray(16)
+    for i in range(16):
+        bits = prefix - 8 * i
+        out[i] = 0xFF if bits >= 8 else (0 if bits <= 0 else (0xFF << (8 - bits)) & 0xFF)
+    return bytes(out)
+
+
+def build_rule_table(rules: np.ndarray) -> np.ndarray:
+    """Final rt->rules after rule_table_add() of `rules` in order: rule_id = insertion index,
+    wildcard (all-zero mask) addresses zeroed for ip_ver 4/6, sorted by (priority, rule_id)."""
+    r = rules.copy()
+    r["rule_id"] = np.arange(len(r), dtype=np.uint32)
+    v4 = r["ip_ver"] == 4
+    v6 = r["ip_ver"] == 6
+    for a, m in (("src_ip", "src_mask"), ("dst_ip", "dst_mask")):
+        mask_v4 = r[m][:, :4].copy().view("<u4").ravel()
+        z4 = v4 & (mask_v4 == 0)
+        r[a][z4, :4] = 0
+        z6 = v6 & ~r[m].any(axis=1)
+        r[a][z6] = 0
+    order = np.lexsort((r["rule_id"], r["priority"]))
+    return r[order]
+
+
+def _set_v4(field: np.ndarray, value: int) -> None:
+    field[:4] = np.frombuffer(np.uint32(value).astype("<u4").tobytes(), np.uint8)
+
+
+def make_rule(priority: int, action: int, *, ip_ver: int | None = None, proto: int = 0,
+              sport: int = 0, dport: int = 0, src=None, dst=None, out_ifindex: int = 1):
+    """One rule_t.  src/dst: (int_v4, prefix) or (bytes16, prefix), like rule_config's
+    parse_ip_prefix (reference src/rule_config.c:38-91): v4 host order, v6 wire bytes.
+    ip_ver=None infers the version from the first address as rule_config_load does
+    (src/rule_config.c:213-227); an explicit 0 keeps a version-agnostic rule (API-only)."""
+    r = np.zeros(1, dtype=RULE_DTYPE)[0]
+    r["priority"] = priority
+    infer = ip_ver is None
+    r["ip_ver"] = 0 if infer else ip_ver
+    r["protocol"] = proto
+    r["src_port"] = sport
+    r["dst_port"] = dport
+    r["action"] = action
+    r["out_ifindex"] = out_ifindex if action == ACT_FWD else 0
+    for name, spec in (("src", src), ("dst", dst)):
+        if spec is None:
+            continue
+        addr, prefix = spec
+        if isinstance(addr, (bytes, bytearray)):
+            r[name + "_ip"][:] = np.frombuffer(bytes(addr), np.uint8)
+            r[name + "_mask"][:] = np.frombuffer(ipv6_mask(prefix), np.uint8)
+            if infer and r["ip_ver"] == 0:
+                r["ip_ver"] = 6
+        else:
+            _set_v4(r[name + "_ip"], addr)
+            _set_v4(r[name + "_mask"], ipv4_mask(prefix))
+            if infer and r["ip_ver"] == 0:
+                r["ip_ver"] = 4
+    return r
+
+
+def rules_array(rules) -> np.ndarray:
+    out = np.zeros(len(rules), dtype=RULE_DTYPE)
+    for i, r in enumerate(rules):
+        out[i] = r
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# neighbour tables: arp_update / ndp_update insertion (reference src/arp_table.c:26-53,
+# src/ndp_table.c:39-65), so slot placement (and probe chains) match a learned table.
+# ---------------------------------------------------------------------------------------------
+
+def ndp_hash(ip16: bytes, cap: int) -> int:
+    w = np.frombuffer(bytes(ip16), "<u4")
+    return int(w[0] ^ w[1] ^ w[2] ^ w[3]) & (cap - 1)
+
+
+def arp_table(cap: int, entries) -> np.ndarray:
+    t = np.zeros(cap, dtype=ARP_DTYPE)
+    for ip, mac in entries:
+        idx = ip & (cap - 1)
+        for i in range(cap):
+            s = (idx + i) & (cap - 1)
+            if not t["valid"][s] or t["ip"][s] == ip:
+                t["valid"][s] = 1
+                t["ip"][s] = ip
+                t["mac"][s] = np.frombuffer(bytes(mac), np.uint8)
+                break
+    return t
+
+
+def ndp_table(cap: int, entries) -> np.ndarray:
+    t = np.zeros(cap, dtype=NDP_DTYPE)
+    for ip, mac in entries:
+        idx = ndp_hash(ip, cap)
+        ipa = np.frombuffer(bytes(ip), np.uint8)
+        for i in range(cap):
+            s = (idx + i) & (cap - 1)
+            if not t["valid"][s] or np.array_equal(t["ip"][s], ipa):
+                t["valid"][s] = 1
+                t["ip"][s] = ipa
+                t["mac"][s] = np.frombuffer(bytes(mac), np.uint8)
+                break
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+# vectorised frame building
+# ---------------------------------------------------------------------------------------------
+
+def _be16(h: np.ndarray, off, val) -> None:
+    val = np.asarray(val, dtype=np.uint32)
+    h[:, off] = (val >> 8) & 0xFF
+    h[:, off + 1] = val & 0xFF
+
+
+def _be32(h: np.ndarray, off, val) -> None:
+    val = np.asarray(val, dtype=np.uint64)
+    for k in range(4):
+        h[:, off + k] = (val >> np.uint64(24 - 8 * k)) & np.uint64(0xFF)
+
+
+def ipv4_header_checksum(h: np.ndarray, ihl: np.ndarray) -> np.ndarray:
+    """Wire checksum of the IPv4 header at byte 14 (RFC 1071), for realistic input frames."""
+    n = h.shape[0]
+    if h.shape[1] < 76:
+        h = np.concatenate([h, np.zeros((n, 76 - h.shape[1]), h.dtype)], axis=1)
+    words = (h[:, 14:74:2].astype(np.uint32) << 8) | h[:, 15:75:2].astype(np.uint32)
+    valid = np.arange(30)[None, :] < (ihl[:, None] * 2)
+    words = np.where(valid, words, 0)
+    words[:, 5] = 0  # checksum field
+    s = words.sum(axis=1)
+    while np.any(s >> 16):
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s & 0xFFFF).astype(np.uint32).reshape(n)
+
+
+def pack_frames(hdr: np.ndarray, lens: np.ndarray, stride: int | None = None,
+                align: int = 16) -> tuple[np.ndarray, np.ndarray]:
+    """Pack header rows (first hdr.shape[1] bytes of each frame; the rest of a frame is zero
+    payload) into one buffer.  Fixed `stride` or variable (len rounded up to `align`)."""
+    n, w = hdr.shape
+    lens = np.asarray(lens, dtype=np.int64)
+    if stride is not None:
+        if np.any(lens > stride):
+            raise ValueError("frame longer than stride")
+        offs = np.arange(n, dtype=np.int64) * stride
+        total = n * stride
+    else:
+        sizes = (lens + align - 1) // align * align
+        sizes = np.maximum(sizes, align)
+        offs = np.zeros(n, dtype=np.int64)
+        np.cumsum(sizes[:-1], out=offs[1:])
+        total = int(offs[-1] + sizes[-1]) if n else 0
+    buf = np.zeros(total + FRAME_TAIL + 128, dtype=np.uint8)
+    keep = np.minimum(lens, w)
+    if stride is not None and stride >= w:
+        view = buf[: n * stride].reshape(n, stride)
+        m = np.arange(w)[None, :] < keep[:, None]
+        view[:, :w] = np.where(m, hdr, 0)
+    else:
+        chunk = 1 << 16
+        cols = np.arange(w)
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            m = cols[None, :] < keep[s:e, None]
+            idx = offs[s:e, None] + cols[None, :]
+            buf[idx[m]] = hdr[s:e][m]
+    return buf, make_desc(offs, lens)
+
+
+def _macs(h: np.ndarray, rng: np.random.Generator) -> None:
+    n = h.shape[0]
+    h[:, 0:6] = rng.integers(0, 256, size=(n, 6), dtype=np.uint8)
+    h[:, 0] &= 0xFE
+    h[:, 6:12] = rng.integers(0, 256, size=(n, 6), dtype=np.uint8)
+    h[:, 6] &= 0xFE
+
+
+def build_ipv4(h, rows, *, src, dst, proto, ttl, ihl, total_len, l4_ports, tcp_doff=None,
+               icmp=None, rng=None):
+    """Fill IPv4 frames in rows of h (wire order)."""
+    hh = h[rows]
+    _be16(hh, 12, 0x0800)
+    hh[:, 14] = 0x40 | ihl
+    hh[:, 15] = 0
+    _be16(hh, 16, total_len)
+    if rng is not None:
+        _be16(hh, 18, rng.integers(0, 65536, size=len(rows)))
+    _be16(hh, 20, 0x4000)
+    hh[:, 22] = ttl
+    hh[:, 23] = proto
+    _be32(hh, 26, src)
+    _be32(hh, 30, dst)
+    # options: NOP padding (0x01) then EOL, as a real stack would emit
+    for extra in np.unique(ihl[ihl > 5]):
+        sel = ihl == extra
+        hh[np.ix_(sel, np.arange(34, 14 + int(extra) * 4))] = 1
+    l4 = 14 + ihl.astype(np.int64) * 4
+    sport, dport = l4_ports
+    r = np.arange(len(rows))
+    for k, val in ((0, sport >> 8), (1, sport & 0xFF), (2, dport >> 8), (3, dport & 0xFF)):
+        hh[r, l4 + k] = val
+    if tcp_doff is not None:
+        hh[r, l4 + 12] = np.where(proto == 6, tcp_doff << 4, hh[r, l4 + 12])
+        hh[r, l4 + 13] = np.where(proto == 6, 0x10, hh[r, l4 + 13])
+    if icmp is not None:
+        itype, icode, iid = icmp
+        isi = proto == 1
+        hh[r[isi], l4[isi]] = itype[isi]
+        hh[r[isi], l4[isi] + 1] = icode[isi]
+        hh[r[isi], l4[isi] + 2] = 0
+        hh[r[isi], l4[isi] + 3] = 0
+        hh[r[isi], l4[isi] + 4] = iid[isi] >> 8
+        hh[r[isi], l4[isi] + 5] = iid[isi] & 0xFF
+    cs = ipv4_header_checksum(hh, ihl.astype(np.int64))
+    _be16(hh, 24, cs)
+    h[rows] = hh
+
+
+def build_ipv6(h, rows, *, src16, dst16, nh, hop, payload_len, sport, dport, tcp_doff=None):
+    hh = h[rows]
+    _be16(hh, 12, 0x86DD)
+    _be32(hh, 14, np.full(len(rows), 0x60000000, dtype=np.uint64))
+    _be16(hh, 18, payload_len)
+    hh[:, 20] = nh
+    hh[:, 21] = hop
+    hh[:, 22:38] = src16
+    hh[:, 38:54] = dst16
+    _be16(hh, 54, sport)
+    _be16(hh, 56, dport)
+    if tcp_doff is not None:
+        hh[:, 66] = np.where(nh == 6, tcp_doff << 4, hh[:, 66])
+        hh[:, 67] = np.where(nh == 6, 0x10, hh[:, 67])
+    h[rows] = hh
+
+
+def _rand_macs(rng, k):
+    m = rng.integers(0, 256, size=(k, 6), dtype=np.uint8)
+    m[:, 0] = (m[:, 0] & 0xFE) | 0x02
+    return m
+
+
+# ---------------------------------------------------------------------------------------------
+# config A — reference rules.example over 64 B UDP/IPv4
+# ---------------------------------------------------------------------------------------------
+
+def rules_example() -> np.ndarray:
+    """reference rules.example:3-25 as rule_config_load would add them (out_iface = lo -> 1)."""
+    return rules_array([
+        make_rule(5, ACT_DROP, proto=6, dport=22),
+        make_rule(1000, ACT_FWD, ip_ver=4, proto=6, src=(0xC0A80000, 16)),
+        make_rule(1200, ACT_FWD, ip_ver=6, src=(bytes.fromhex("20010db8") + bytes(12), 32)),
+        make_rule(9999, ACT_DROP),
+    ])
+
+
+def _udp64(n, rng, dst_pool):
+    h = np.zeros((n, 64), dtype=np.uint8)
+    _macs(h, rng)
+    src = (np.uint64(0x0A000000) + rng.integers(0, 1 << 24, size=n).astype(np.uint64))
+    dst = dst_pool[rng.integers(0, len(dst_pool), size=n)].astype(np.uint64)
+    sport = rng.integers(1, 65536, size=n).astype(np.uint32)
+    dport = rng.integers(1, 65536, size=n).astype(np.uint32)
+    return h, src, dst, sport, dport
+
+
+def config_a(n: int = 10_000, seed: int = 1) -> Workload:
+    rng = np.random.default_rng(seed)
+    dst_pool = np.uint64(0x0A800000) + np.arange(256, dtype=np.uint64)
+    h, src, dst, sport, dport = _udp64(n, rng, dst_pool)
+    rows = np.arange(n)
+    build_ipv4(h, rows, src=src, dst=dst, proto=np.full(n, 17), ttl=np.full(n, 64),
+               ihl=np.full(n, 5), total_len=np.full(n, 50), l4_ports=(sport, dport), rng=rng)
+    _be16(h, 38, np.full(n, 30))
+    frames, desc = pack_frames(h, np.full(n, 64), stride=64)
+    return Workload("A", frames, desc, rules_example(), 1024,
+                    np.zeros(1024, ARP_DTYPE), np.zeros(1024, NDP_DTYPE))
+
+
+# ---------------------------------------------------------------------------------------------
+# config B — 1M x 64 B UDP/IPv4, 8 rules exercising every field type
+# ---------------------------------------------------------------------------------------------
+
+def rules_b() -> np.ndarray:
+    """Eight rules, inserted out of priority order so the (priority, rule_id) sort matters."""
+    return rules_array([
+        make_rule(9999, ACT_DROP),                                            # catch-all
+        make_rule(40, ACT_FWD, dst=(0x0A800000, 25)),                         # v4 dst /25
+        make_rule(10, ACT_FWD, dport=53),                                     # port only
+        make_rule(20, ACT_DROP, src=(0x0A010000, 16)),                        # v4 src /16
+        make_rule(30, ACT_DROP, proto=6, dport=22),                           # never (all UDP)
+        make_rule(50, ACT_FWD, src=(bytes.fromhex("20010db8") + bytes(12), 32)),  # v6 only
+        make_rule(60, ACT_DROP, sport=1234),                                  # port only
+        make_rule(70, ACT_DROP, proto=1),                                     # icmp
+    ])
+
+
+def neigh_b(rng) -> np.ndarray:
+    """ARP: 240 of the 256 hosts of 10.128.0.0/24, after 64 colliding hosts of 10.129.0.0/24
+    (same low 10 bits, so lookups walk probe chains as in a learned table)."""
+    ents = []
+    for x in rng.permutation(256)[:64]:
+        ents.append((0x0A810000 + int(x), _rand_macs(rng, 1)[0].tobytes()))
+    for x in rng.permutation(256)[:240]:
+        ents.append((0x0A800000 + int(x), _rand_macs(rng, 1)[0].tobytes()))
+    return arp_table(1024, ents)
+
+
+def config_b(n: int = 1 << 20, seed: int = 2) -> Workload:
+    rng = np.random.default_rng(seed)
+    arp = neigh_b(rng)
+    dst_pool = np.uint64(0x0A800000) + np.arange(256, dtype=np.uint64)
+    h, src, dst, sport, dport = _udp64(n, rng, dst_pool)
+    dport = np.where(rng.integers(0, 8, size=n) == 0, 53, dport).astype(np.uint32)
+    sport = np.where(rng.integers(0, 64, size=n) == 0, 1234, sport).astype(np.uint32)
+    ttl = rng.integers(1, 65, size=n)
+    rows = np.arange(n)
+    build_ipv4(h, rows, src=src, dst=dst, proto=np.full(n, 17), ttl=ttl, ihl=np.full(n, 5),
+               total_len=np.full(n, 50), l4_ports=(sport, dport), rng=rng)
+    _be16(h, 38, np.full(n, 30))
+    frames, desc = pack_frames(h, np.full(n, 64), stride=64)
+    return Workload("B", frames, desc, rules_b(), 1024, arp, np.zeros(1024, NDP_DTYPE))
+
+
+# ---------------------------------------------------------------------------------------------
+# config C — IMIX, v4+v6, 1k 5-tuple rules, ARP + NDP
+# ---------------------------------------------------------------------------------------------
+
+def _v6_pool(rng, k, prefix=bytes.fromhex("20010db8")):
+    tail = rng.integers(0, 256, size=(k, 12), dtype=np.uint8)
+    tail[:, :6] = rng.integers(0, 4, size=(k, 6), dtype=np.uint8)  # clustered subnets
+    pre = np.frombuffer(prefix, np.uint8)[None, :].repeat(k, axis=0)
+    return np.concatenate([pre, tail], axis=1)
+
+
+def _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, protos4, protos6, ports,
+                 exact_frac=0.0):
+    """Random 5-tuple rules drawn from the traffic's own pools so they match at spread-out
+    positions; last rule is the catch-all."""
+    rules = []
+    prios = rng.permutation(n_rules - 1) + 1
+    for i in range(n_rules - 1):
+        is6 = rng.random() < 0.3
+        act = ACT_FWD if rng.random() < 0.5 else ACT_DROP
+        exact = rng.random() < exact_frac
+        kw = {}
+        if is6:
+            kw["ip_ver"] = 6
+            if exact or rng.random() < 0.7:
+                kw["src"] = (bytes(v6_src[rng.integers(len(v6_src))]),
+                             128 if exact else int(rng.integers(32, 129)))
+            if exact or rng.random() < 0.7:
+                kw["dst"] = (bytes(v6_dst[rng.integers(len(v6_dst))]),
+                             128 if exact else int(rng.integers(32, 129)))
+            if exact or rng.random() < 0.5:
+                kw["proto"] = int(rng.choice(protos6))
+        else:
+            kw["ip_ver"] = 4
+            if exact or rng.random() < 0.7:
+                kw["src"] = (int(v4_src[rng.integers(len(v4_src))]),
+                             32 if exact else int(rng.integers(8, 33)))
+            if exact or rng.random() < 0.7:
+                kw["dst"] = (int(v4_dst[rng.integers(len(v4_dst))]),
+                             32 if exact else int(rng.integers(8, 33)))
+            if exact or rng.random() < 0.5:
+                kw["proto"] = int(rng.choice(protos4))
+        if exact or rng.random() < 0.3:
+            kw["sport"] = int(ports[rng.integers(len(ports))])
+        if exact or rng.random() < 0.4:
+            kw["dport"] = int(ports[rng.integers(len(ports))])
+        if rng.random() < 0.1 and not exact:
+            kw["ip_ver"] = 0  # version-agnostic: address bytes apply under both views
+        rules.append(make_rule(int(prios[i]), act, **kw))
+    rules.append(make_rule(1 << 30, ACT_DROP))
+    return rules_array(rules)
+
+
+def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024) -> Workload:
+    rng = np.random.default_rng(seed)
+    n_hosts = 1000
+    v4_src = (0x0A000000 + rng.integers(0, 1 << 16, size=n_hosts) * 7).astype(np.uint64)
+    v4_dst = (0xAC100000 + rng.integers(0, 1 << 12, size=n_hosts)).astype(np.uint64)
+    v6_src = _v6_pool(rng, n_hosts)
+    v6_dst = _v6_pool(rng, n_hosts, prefix=bytes.fromhex("2001db80"))
+    ports = np.concatenate([np.array([53, 80, 443, 22, 123, 8080]),
+                            rng.integers(1024, 65536, size=200)])
+    arp = arp_table(1024, [(int(ip), _rand_macs(rng, 1)[0].tobytes())
+                           for ip in v4_dst[rng.permutation(n_hosts)[:600]]])
+    ndp = ndp_table(1024, [(bytes(ip), _rand_macs(rng, 1)[0].tobytes())
+                           for ip in v6_dst[rng.permutation(n_hosts)[:600]]])
+    rules = _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, [17, 6, 1], [17, 6], ports)
+
+    size = rng.choice(np.array([64, 570, 1518]), size=n, p=[7 / 12, 4 / 12, 1 / 12])
+    is6 = rng.random(n) < 0.3
+    h = np.zeros((n, 128), dtype=np.uint8)
+    _macs(h, rng)
+    sport = ports[rng.integers(0, len(ports), size=n)].astype(np.uint32)
+    dport = ports[rng.integers(0, len(ports), size=n)].astype(np.uint32)
+    r4 = np.nonzero(~is6)[0]
+    r6 = np.nonzero(is6)[0]
+    p4 = rng.choice(np.array([17, 6, 1]), size=len(r4), p=[0.5, 0.4, 0.1])
+    itype = rng.choice(np.array([0, 8, 3, 11]), size=len(r4)).astype(np.uint32)
+    icode = rng.integers(0, 4, size=len(r4)).astype(np.uint32)
+    build_ipv4(h, r4, src=v4_src[rng.integers(0, n_hosts, size=len(r4))],
+               dst=v4_dst[rng.integers(0, n_hosts, size=len(r4))], proto=p4,
+               ttl=rng.integers(1, 129, size=len(r4)), ihl=np.full(len(r4), 5),
+               total_len=size[r4] - 14, l4_ports=(sport[r4], dport[r4]),
+               tcp_doff=np.full(len(r4), 5), icmp=(itype, icode, sport[r4]), rng=rng)
+    p6 = rng.choice(np.array([17, 6]), size=len(r6))
+    build_ipv6(h, r6, src16=v6_src[rng.integers(0, n_hosts, size=len(r6))],
+               dst16=v6_dst[rng.integers(0, n_hosts, size=len(r6))], nh=p6,
+               hop=rng.integers(1, 129, size=len(r6)), payload_len=size[r6] - 54,
+               sport=sport[r6], dport=dport[r6], tcp_doff=np.full(len(r6), 5))
+    frames, desc = pack_frames(h, size)
+    return Workload("C", frames, desc, rules, n_rules, arp, ndp)
+
+
+# ---------------------------------------------------------------------------------------------
+# config D — 64k rules, variable-length headers, malformed traffic, v4/v6 interleaved
+# ---------------------------------------------------------------------------------------------
+
+def config_d(n: int = 1 << 24, seed: int = 4, n_rules: int = 1 << 16) -> Workload:
+    rng = np.random.default_rng(seed)
+    n_flows = n_rules - 1
+    # one exact flow per rule so first-match positions spread uniformly over the table
+    f6 = rng.random(n_flows) < 0.3
+    f_src4 = (0x0B000000 + rng.integers(0, 1 << 24, size=n_flows)).astype(np.uint64)
+    f_dst4 = (0xAC100000 + rng.integers(0, 1 << 12, size=n_flows)).astype(np.uint64)
+    f_src6 = _v6_pool(rng, n_flows)
+    f_dst6 = _v6_pool(rng, n_flows, prefix=bytes.fromhex("2001db80"))
+    f_proto = np.where(f6, rng.choice(np.array([17, 6]), size=n_flows),
+                       rng.choice(np.array([17, 6, 1]), size=n_flows))
+    f_sport = rng.integers(1, 65536, size=n_flows).astype(np.uint32)
+    f_dport = rng.integers(1, 65536, size=n_flows).astype(np.uint32)
+    f_dport = np.where(f_proto == 1, (8 << 8) | 0, f_dport)  # echo request type/code
+    prios = rng.permutation(n_flows) + 1
+    acts = np.where(rng.random(n_flows) < 0.5, ACT_FWD, ACT_DROP)
+
+    rules = np.zeros(n_rules, dtype=RULE_DTYPE)
+    rules["priority"][:n_flows] = prios
+    rules["ip_ver"][:n_flows] = np.where(f6, 6, 4)
+    rules["protocol"][:n_flows] = f_proto
+    rules["src_port"][:n_flows] = f_sport
+    rules["dst_port"][:n_flows] = f_dport
+    rules["action"][:n_flows] = acts
+    rules["out_ifindex"][:n_flows] = np.where(acts == ACT_FWD, 1, 0)
+    v4r = np.nonzero(~f6)[0]
+    v6r = np.nonzero(f6)[0]
+    rules["src_ip"][v4r, :4] = f_src4[v4r].astype("<u4").view(np.uint8).reshape(-1, 4)
+    rules["dst_ip"][v4r, :4] = f_dst4[v4r].astype("<u4").view(np.uint8).reshape(-1, 4)
+    rules["src_mask"][v4r, :4] = 0xFF
+    rules["dst_mask"][v4r, :4] = 0xFF
+    rules["src_ip"][v6r] = f_src6[v6r]
+    rules["dst_ip"][v6r] = f_dst6[v6r]
+    rules["src_mask"][v6r] = 0xFF
+    rules["dst_mask"][v6r] = 0xFF
+    # ~1 % wildcard rules (port-only / prefix) sprinkled in, they shadow some flows
+    wild = rng.permutation(n_flows)[: n_flows // 100]
+    rules["src_port"][wild] = 0
+    rules["src_mask"][wild, 2:] = 0
+    rules["src_ip"][wild, 2:] = 0
+    rules["priority"][n_rules - 1] = 1 << 30
+    rules["action"][n_rules - 1] = ACT_DROP
+
+    arp = arp_table(1024, [(int(ip), _rand_macs(rng, 1)[0].tobytes())
+                           for ip in np.unique(f_dst4[v4r])[:600]])
+    ndp = ndp_table(1024, [(bytes(f_dst6[i]), _rand_macs(rng, 1)[0].tobytes())
+                           for i in v6r[:600]])
+
+    flow = rng.integers(0, n_flows, size=n)
+    # 5 % of packets hit no specific rule (random 5-tuple -> catch-all, the longest scans)
+    stray = rng.random(n) < 0.05
+    is6 = f6[flow]
+    h = np.zeros((n, 128), dtype=np.uint8)
+    _macs(h, rng)
+    proto = f_proto[flow].copy()
+    sport = np.where(stray, rng.integers(1, 65536, size=n), f_sport[flow]).astype(np.uint32)
+    dport = f_dport[flow].astype(np.uint32)
+    r4 = np.nonzero(~is6)[0]
+    r6 = np.nonzero(is6)[0]
+    ihl = np.where(rng.random(len(r4)) < 0.5, 5, rng.integers(6, 16, size=len(r4)))
+    doff4 = np.where(rng.random(len(r4)) < 0.5, 5, rng.integers(6, 16, size=len(r4)))
+    l4len4 = np.where(proto[r4] == 6, doff4 * 4, 8)
+    len4 = 14 + ihl * 4 + l4len4 + rng.integers(0, 8, size=len(r4))
+    build_ipv4(h, r4, src=f_src4[flow[r4]], dst=f_dst4[flow[r4]], proto=proto[r4],
+               ttl=rng.integers(1, 65, size=len(r4)), ihl=ihl, total_len=len4 - 14,
+               l4_ports=(sport[r4], dport[r4]), tcp_doff=doff4,
+               icmp=(np.full(len(r4), 8), np.zeros(len(r4), dtype=np.int64), sport[r4]),
+               rng=rng)
+    doff6 = np.where(rng.random(len(r6)) < 0.5, 5, rng.integers(6, 15, size=len(r6)))
+    l4len6 = np.where(proto[r6] == 6, doff6 * 4, 8)
+    len6 = 54 + l4len6 + rng.integers(0, 8, size=len(r6))
+    build_ipv6(h, r6, src16=f_src6[flow[r6]], dst16=f_dst6[flow[r6]], nh=proto[r6],
+               hop=rng.integers(1, 65, size=len(r6)), payload_len=len6 - 54,
+               sport=sport[r6], dport=dport[r6], tcp_doff=doff6)
+    lens = np.zeros(n, dtype=np.int64)
+    lens[r4] = len4
+    lens[r6] = len6
+    lens = np.minimum(lens, 128)
+    # 10 % malformed, one of several failure modes each
+    bad = np.nonzero(rng.random(n) < 0.10)[0]
+    mode = rng.integers(0, 8, size=len(bad))
+    for m in range(8):
+        rows = bad[mode == m]
+        if m == 0:    # truncated somewhere inside the headers
+            lens[rows] = rng.integers(0, np.maximum(lens[rows] - 1, 1))
+        elif m == 1:  # wrong IPv4 version nibble
+            h[rows, 14] = np.where(h[rows, 12] == 0x08, (h[rows, 14] & 0x0F) | 0x50, h[rows, 14])
+        elif m == 2:  # VLAN tag ethertype
+            h[rows, 12] = 0x81
+            h[rows, 13] = 0x00
+        elif m == 3:  # GRE / ESP
+            h[rows, 23] = np.where(h[rows, 12] == 0x08, rng.choice([47, 50], size=len(rows)),
+                                   h[rows, 23])
+            h[rows, 20] = np.where(h[rows, 12] == 0x86, rng.choice([47, 50], size=len(rows)),
+                                   h[rows, 20])
+        elif m == 4:  # ICMPv6 (not NS/NA) on IPv6 rows, IHL < 5 on IPv4 rows
+            h[rows, 20] = np.where(h[rows, 12] == 0x86, 58, h[rows, 20])
+            h[rows, 54] = np.where(h[rows, 12] == 0x86, 128, h[rows, 54])
+            h[rows, 14] = np.where(h[rows, 12] == 0x08, 0x44, h[rows, 14])
+        elif m == 5:  # TCP data offset < 5
+            sel4 = (h[rows, 12] == 0x08) & (h[rows, 23] == 6)
+            l4 = 14 + (h[rows, 14] & 0x0F).astype(np.int64) * 4
+            h[rows[sel4], l4[sel4] + 12] = 0x30
+            sel6 = (h[rows, 12] == 0x86) & (h[rows, 20] == 6)
+            h[rows[sel6], 66] = 0x20
+        elif m == 6:  # TTL / hop limit 0
+            h[rows, 22] = np.where(h[rows, 12] == 0x08, 0, h[rows, 22])
+            h[rows, 21] = np.where(h[rows, 12] == 0x86, 0, h[rows, 21])
+        else:         # IHL larger than the frame
+            h[rows, 14] = np.where(h[rows, 12] == 0x08, 0x4F, h[rows, 14])
+            lens[rows] = np.where(h[rows, 12] == 0x08, np.minimum(lens[rows], 60), lens[rows])
+    frames, desc = pack_frames(h, lens, stride=128)
+    return Workload("D", frames, desc, rules, n_rules, arp, ndp)
+
+
+CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d}
+
+
+def make(name: str, n: int | None = None, seed: int | None = None, **kw) -> Workload:
+    fn = CONFIGS[name]
+    args = {}
+    if n is not None:
+        args["n"] = n
+    if seed is not None:
+        args["seed"] = seed
+    args.update(kw)
+    return fn(**args)
+
+
+# ---------------------------------------------------------------------------------------------
+# edge cases — every parse gate, control packet kind and quirk of SURVEY.md §8.1
+# ---------------------------------------------------------------------------------------------
+
+def _frame(*parts) -> bytes:
+    return b"".join(parts)
+
+
+def _eth(et: int, dst=b"\x00\x11\x22\x33\x44\x55", src=b"\x66\x77\x88\x99\xaa\xbb") -> bytes:
+    return dst + src + et.to_bytes(2, "big")
+
+
+def _ip4(proto, src, dst, ttl=64, ihl=5, ver=4, total=0, opts=None) -> bytes:
+    opt = bytes(opts) if opts is not None else b"\x01" * (ihl * 4 - 20)
+    hdr = bytes([(ver << 4) | ihl, 0]) + total.to_bytes(2, "big") + b"\x12\x34\x40\x00" + \
+        bytes([ttl, proto]) + b"\x00\x00" + src.to_bytes(4, "big") + dst.to_bytes(4, "big") + opt
+    return hdr
+
+
+def _ip6(nh, src16, dst16, hop=64, plen=0) -> bytes:
+    return (0x60000000).to_bytes(4, "big") + plen.to_bytes(2, "big") + bytes([nh, hop]) + \
+        bytes(src16) + bytes(dst16)
+
+
+def _udp(sp, dp) -> bytes:
+    return sp.to_bytes(2, "big") + dp.to_bytes(2, "big") + b"\x00\x08\x00\x00"
+
+
+def _tcp(sp, dp, doff=5) -> bytes:
+    return sp.to_bytes(2, "big") + dp.to_bytes(2, "big") + b"\x00" * 8 + bytes([doff << 4, 0x10]) + \
+        b"\xff\xff\x00\x00\x00\x00" + b"\x00" * max(0, doff * 4 - 20)
+
+
+def _icmp(t, c, ident) -> bytes:
+    return bytes([t, c, 0, 0]) + ident.to_bytes(2, "big") + b"\x00\x01"
+
+
+def _arp(op, sha, spa, tha, tpa, htype=1, ptype=0x0800, hlen=6, plen=4) -> bytes:
+    return htype.to_bytes(2, "big") + ptype.to_bytes(2, "big") + bytes([hlen, plen]) + \
+        op.to_bytes(2, "big") + bytes(sha) + spa.to_bytes(4, "big") + bytes(tha) + \
+        tpa.to_bytes(4, "big")
+
+
+def edge_frames():
+    """(frame bytes, length) pairs; length may cut the frame short (truncation gates)."""
+    V6A = bytes.fromhex("20010db8000000000000000000000001")
+    V6B = bytes.fromhex("20010db8000000000000000000000002")
+    V6N = bytes.fromhex("2001db80000000000000000000000abc")  # in NDP table
+    ZERO6 = bytes(16)
+    MAC = bytes.fromhex("0a0b0c0d0e0f")
+    out = []
+
+    def add(fr, ln=None):
+        out.append((fr, len(fr) if ln is None else ln))
+
+    v4u = _frame(_eth(0x0800), _ip4(17, 0x0A000001, 0x0A800005), _udp(1000, 53))
+    for ln in range(0, len(v4u) + 1):                       # every truncation of a UDP frame
+        add(v4u, ln)
+    v4t = _frame(_eth(0x0800), _ip4(6, 0x0A000001, 0x0A800006), _tcp(2000, 22))
+    for ln in (53, 54, 60):
+        add(v4t, ln)
+    for doff in (0, 4, 5, 6, 15):                            # TCP data offset gates
+        add(_frame(_eth(0x0800), _ip4(6, 0x0A000002, 0x0A800007), _tcp(2000, 80, doff=max(doff, 5))[:12] +
+                   bytes([doff << 4]) + b"\x10" + b"\x00" * 6 + b"\x00" * 40), 14 + 20 + 20 + 16)
+    for ihl in (0, 4, 5, 6, 10, 15):                         # IHL gates and options
+        ih = max(ihl, 5)
+        f = _frame(_eth(0x0800), _ip4(17, 0x0A000003, 0x0A800008, ihl=ih), _udp(7, 8))
+        f = f[:14] + bytes([0x40 | ihl]) + f[15:]
+        add(f)
+        add(f, 14 + ih * 4 + 4)
+    add(_frame(_eth(0x0800), _ip4(17, 0x0A000003, 0x0A800008, ver=6), _udp(7, 8)))  # ver != 4
+    for t, c in ((8, 0), (0, 0), (3, 1), (11, 0)):            # ICMP: id->sport, type<<8|code
+        add(_frame(_eth(0x0800), _ip4(1, 0x0A000004, 0x0A800009), _icmp(t, c, 0x1234)))
+    add(_frame(_eth(0x0800), _ip4(1, 0x0A000004, 0x0A800009), _icmp(8, 0, 1)), 38)
+    for proto in (47, 50, 58, 0, 255):                        # unknown L4 protocols
+        add(_frame(_eth(0x0800), _ip4(proto, 0x0A000005, 0x0A80000A), _udp(1, 2)))
+    for ttl in (0, 1, 2, 255):                                # TTL edge cases on FWD
+        add(_frame(_eth(0x0800), _ip4(17, 0x0A000006, 0x0A800005, ttl=ttl), _udp(5, 53)))
+    add(_frame(_eth(0x0800), _ip4(17, 0x0A000006, 0x0A8000C8), _udp(5, 53)))  # ARP miss -> FWD
+    add(_frame(_eth(0x0800), _ip4(17, 0x0A000006, 0x00000000), _udp(5, 53)))  # dst 0.0.0.0
+    add(_frame(_eth(0x0800), _ip4(6, 0xC0A80101, 0x0A800005, ihl=7), _tcp(5, 443, doff=8)))
+    # IPv6
+    v6u = _frame(_eth(0x86DD), _ip6(17, V6A, V6N), _udp(3000, 53))
+    for ln in (53, 54, 61, 62, 70):
+        add(v6u, ln)
+    add(_frame(_eth(0x86DD), _ip6(6, V6A, V6B), _tcp(4000, 443)))
+    add(_frame(_eth(0x86DD), _ip6(6, V6A, V6B), _tcp(4000, 443)), 73)
+    add(_frame(_eth(0x86DD), _ip6(6, V6A, V6B), _tcp(4000, 443, doff=6)), 78)
+    for hop in (0, 1, 2):
+        add(_frame(_eth(0x86DD), _ip6(17, V6A, V6N, hop=hop), _udp(9, 53)))
+    add(_frame(_eth(0x86DD), _ip6(17, V6A, ZERO6), _udp(9, 53)))        # dst :: (quirk 15)
+    add(_frame(_eth(0x86DD), _ip6(17, V6B, ZERO6), _udp(9, 53)))
+    add(_frame(_eth(0x86DD), _ip6(1, V6A, V6B), _icmp(128, 0, 7)))      # ICMP (proto 1) in v6
+    v6n = _frame(_eth(0x86DD), _ip6(17, V6A, V6N), _udp(3000, 53))
+    add(v6n[:14] + bytes([0x40]) + v6n[15:])                            # v6 version not checked
+    add(_frame(_eth(0x86DD), _ip6(58, V6A, V6B), bytes([128, 0, 0, 0]) + b"\x00" * 20))  # echo
+    # NDP: NS with SLLA, NA with TLLA, short ones (dropped as parse failures), no option
+    ns = _frame(_eth(0x86DD), _ip6(58, V6A, V6B), bytes([135, 0, 0, 0, 0, 0, 0, 0]) + V6B,
+                bytes([1, 1]) + MAC)
+    na = _frame(_eth(0x86DD), _ip6(58, V6B, V6A), bytes([136, 0, 0, 0, 0x60, 0, 0, 0]) + V6N,
+                bytes([2, 1]) + bytes.fromhex("a1a2a3a4a5a6"))
+    add(ns)
+    add(na)
+    add(ns, 77)
+    add(ns, 78)
+    add(_frame(_eth(0x86DD), _ip6(58, V6A, V6B), bytes([136, 0, 0, 0, 0, 0, 0, 0]) + V6N,
+               bytes([5, 0]) + b"\x00" * 6))                            # zero-length option
+    # ARP: request for our IP (reply in place), request for another IP, reply, malformed
+    add(_frame(_eth(0x0806, dst=b"\xff" * 6), _arp(1, MAC, 0x0A800063, bytes(6), PORT_IP4)))
+    add(_frame(_eth(0x0806, dst=b"\xff" * 6), _arp(1, MAC, 0x0A800064, bytes(6), 0x0A800001)))
+    add(_frame(_eth(0x0806), _arp(2, bytes.fromhex("0c0c0c0c0c0c"), 0x0A800005, MAC, PORT_IP4)))
+    add(_frame(_eth(0x0806), _arp(1, MAC, 0x0A800065, bytes(6), PORT_IP4, hlen=8)))
+    add(_frame(_eth(0x0806), _arp(1, MAC, 0x0A800066, bytes(6), PORT_IP4)), 30)  # short ARP
+    add(_frame(_eth(0x0806), _arp(1, MAC, 0x0A800067, bytes(6), PORT_IP4 & 0xFFFF0000)), 40)
+    add(_frame(_eth(0x0806)), 14)
+    # other ethertypes
+    add(_frame(_eth(0x8100), b"\x00\x01\x08\x00", _ip4(17, 1, 2), _udp(1, 2)))
+    add(_frame(_eth(0x88CC), b"\x00" * 40))
+    add(b"\x00" * 12 + b"\x08", 13)
+    add(b"", 0)
+    return out
+
+
+def edge_rules() -> np.ndarray:
+    V6P = bytes.fromhex("20010db8") + bytes(12)
+    return rules_array([
+        make_rule(9999, ACT_DROP),
+        make_rule(10, ACT_FWD, dport=53),
+        make_rule(20, ACT_DROP, proto=6, dport=22),
+        make_rule(30, ACT_FWD, ip_ver=4, proto=6, src=(0xC0A80000, 16)),
+        make_rule(40, ACT_DROP, proto=1, sport=0x1234, dport=0x0800),
+        make_rule(50, 2, proto=1),                                   # unknown action type
+        make_rule(60, ACT_FWD, ip_ver=6, src=(V6P, 32)),
+        # version-0 rule with a v6 address: its bytes 0-3 also apply to v4 packets
+        make_rule(70, ACT_DROP, ip_ver=0, dst=(bytes.fromhex("0a800008") + bytes(12), 40)),
+        make_rule(15, ACT_FWD, ip_ver=4, dst=(bytes.fromhex("2001db80") + bytes(12), 128)),
+        make_rule(80, ACT_FWD, proto=6),
+    ])
+
+
+def config_edge(repeat: int = 4, seed: int = 5) -> Workload:
+    """The edge frames, repeated in a shuffled order, with tables that make both neighbour
+    cache paths (hit, miss, starting-entry disagreement) reachable."""
+    rng = np.random.default_rng(seed)
+    fr = edge_frames()
+    order = np.concatenate([np.arange(len(fr))] + [rng.permutation(len(fr)) for _ in range(repeat - 1)])
+    frames_b = [fr[i] for i in order]
+    lens = np.array([ln for _, ln in frames_b], dtype=np.int64)
+    h = np.zeros((len(frames_b), 128), dtype=np.uint8)
+    for i, (f, _) in enumerate(frames_b):
+        b = np.frombuffer(f[:128], np.uint8)
+        h[i, : len(b)] = b
+    # store the whole frame bytes (not just `len`): bytes past len must be ignored
+    frames, desc = pack_frames(h, np.maximum(lens, 0))
+    arp = arp_table(16, [(0x0A800005, bytes.fromhex("aabbccdd0005")),
+                         (0x0A800015, bytes.fromhex("aabbccdd0015")),   # same slot as .5
+                         (0x0A800006, bytes.fromhex("aabbccdd0006")),
+                         (0x00000000, bytes.fromhex("aabbccdd0000"))])
+    ndp = ndp_table(16, [(bytes.fromhex("2001db80000000000000000000000abc"),
+                          bytes.fromhex("bbccddee0abc")),
+                         (bytes.fromhex("20010db8000000000000000000000002"),
+                          bytes.fromhex("bbccddee0002"))])
+    return Workload("edge", frames, desc, edge_rules(), 64, arp, ndp)
