@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+EVENT_EVERY = 8   # sample the kernel events on every 8th timed step
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
 WORKLOADS = {
     "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",
@@ -95,8 +96,8 @@ def cpu_baseline(wl, threads: int) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="B", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=None, help="override batch size")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -154,7 +155,11 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     v_first = verdict.cpu().numpy().view(np.uint32).copy()  # warm-up batch 0 verdicts
 
-    worker.timing_enable(True)
+    # Kernel timing events ride along in the timed region on every EVENT_EVERY-th step: each
+    # event is a queue packet of its own (a few us), so timing every step would tax the very
+    # throughput being measured.  UPE_BENCH_EVENTS=0: diagnostic run without them.
+    events = os.environ.get("UPE_BENCH_EVENTS", "1") != "0"
+    worker.timing_enable(EVENT_EVERY if events else 0)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -182,7 +187,7 @@ def main() -> None:
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first)
         bytes_per_launch = float(bpp.sum())
-        kern_s = classify_ms / max(launches, 1) / 1e3
+        kern_s = classify_ms / launches / 1e3 if launches else float("nan")
         achieved = bytes_per_launch / kern_s / 1e9
         ms_step = elapsed / args.steps * 1e3
         out = {
@@ -214,6 +219,7 @@ def main() -> None:
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "algorithmic_bytes_per_packet": round(bytes_per_launch / n, 2),
                 "kernel_mpps": round(n / kern_s / 1e6, 1),
+                "event_samples": int(launches),
             },
         }
         if not args.no_cpu_baseline:

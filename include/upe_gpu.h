@@ -222,9 +222,11 @@ int upe_gpu_get_stats(upe_gpu_ctx_t *ctx, upe_counters_t *counters, upe_rule_sta
                       size_t capacity);
 int upe_gpu_reset_stats(upe_gpu_ctx_t *ctx);
 
-/* Kernel timing.  While enabled, every upe_gpu_process() records HIP events on its stream
- * around the classify kernel and the finalize kernel.  upe_gpu_timing_read() synchronises and
- * returns the summed durations (ms) and the number of process() calls since enabling. */
+/* Kernel timing.  enable = k > 0: every k-th upe_gpu_process() call (the first, then every k-th)
+ * records HIP events on its stream around each of its two launches (classify: one workgroup per
+ * 256-packet tile; finalize: the batch-wide fold); sampling keeps the events' own queue cost out
+ * of a throughput run.  enable = 0 turns timing off.  upe_gpu_timing_read() synchronises and
+ * returns the summed time (ms) of each kernel over the timed calls and their number. */
 int upe_gpu_timing_enable(upe_gpu_ctx_t *ctx, int enable);
 int upe_gpu_timing_read(upe_gpu_ctx_t *ctx, double *classify_ms, double *finalize_ms,
                         uint64_t *launches);

@@ -230,3 +230,31 @@ def test_config_d_full_properties(gpu_worker_factory):
         v = verdict[start:start + 4096]
         # verdict code, rule index and the TTL/checksum rewrite do not depend on L1 history
         assert np.array_equal(v & 0xFFFFFF0F, r.verdict & 0xFFFFFF0F)
+
+
+@pytest.mark.parametrize("first_hit", [None, 0, 777, 150_001, 299_999])
+def test_lookback_far_first_hit(gpu_worker_factory, first_hit):
+    """A starting ARP entry that disagrees with the table and a batch aimed at it: every packet
+    before the first miss-then-hit packet (placed far into the batch, or absent) must take the
+    entry's MAC — the decoupled look-back across ~1200 tiles."""
+    from upe_amd.layout import desc_offsets
+
+    wl = synth.config_b(n=300_000, seed=12)
+    ip0 = 0x0A800007
+    l1 = synth.l1_zero()
+    l1["last_arp_ip"] = ip0
+    l1["last_arp_mac"] = np.frombuffer(bytes.fromhex("0badc0ffee01"), np.uint8)
+    wl.l1 = l1
+    offs = desc_offsets(wl.desc)
+    dst = np.frombuffer(ip0.to_bytes(4, "big"), np.uint8)
+    wl.frames[(offs[:, None] + np.arange(30, 34)[None, :]).ravel()] = np.tile(dst, wl.n)
+    if first_hit is not None:
+        other = np.frombuffer((0x0A800000 + int(wl.arp["ip"][wl.arp["valid"] == 1][0] & 0xFF))
+                              .to_bytes(4, "big"), np.uint8)
+        wl.frames[offs[first_hit] + 30:offs[first_hit] + 34] = other
+        wl.frames[offs[first_hit] + 22] = 64     # TTL alive
+        wl.frames[offs[first_hit] + 36:offs[first_hit] + 38] = [0, 53]  # dport 53 -> FWD rule
+    r = oracle.run_restated(wl)
+    got = _run(gpu_worker_factory, wl)
+    _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
+                       "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")

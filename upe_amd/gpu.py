@@ -19,7 +19,8 @@ import numpy as np
 from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, L1_DTYPE, NDP_DTYPE,
                      RULE_DTYPE, RULE_STAT_DTYPE)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")
+LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")  # override: diagnostic builds only
 
 
 class UpeGpuError(RuntimeError):
@@ -181,8 +182,9 @@ class GpuWorker:
         _check(LIB.upe_gpu_reset_stats(self._ctx), "upe_gpu_reset_stats")
 
     # ---- kernel timing (HIP events on the launch stream) ----
-    def timing_enable(self, on: bool = True) -> None:
-        _check(LIB.upe_gpu_timing_enable(self._ctx, int(on)), "upe_gpu_timing_enable")
+    def timing_enable(self, every: int = 1) -> None:
+        """Record kernel events on every ``every``-th process() call (0 / False: off)."""
+        _check(LIB.upe_gpu_timing_enable(self._ctx, int(every)), "upe_gpu_timing_enable")
 
     def timing_read(self):
         a, b = ctypes.c_double(), ctypes.c_double()
