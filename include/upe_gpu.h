@@ -150,8 +150,9 @@ enum {
 /* frames : one device buffer holding the frames back to back.  Every frame starts on a 16-byte
  *          boundary, and at least UPE_FRAME_TAIL readable bytes must follow each frame start
  *          (pad the buffer end).  Bytes at or beyond a frame's length are never used.
- * desc[i]: (byte_offset << 16) | len, len <= 65535.  A frame may be a header window shorter
- *          than len as long as it holds the first min(len, UPE_HDR_WINDOW) bytes.
+ * desc[i]: (byte_offset << 16) | len, len <= 65535, byte_offset a multiple of 16 below 2^36.
+ *          A frame may be a header window shorter than len as long as it holds the first
+ *          min(len, UPE_HDR_WINDOW) bytes.
  * verdict: n uint32 words, written by the kernel.
  * A batch is one constant-table segment: control packets (ARP, NDP NS/NA) in it are classified
  * exactly, but their table updates are applied by the caller after the batch (split batches at

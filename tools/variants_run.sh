@@ -1,6 +1,7 @@
 #!/bin/bash
-# Diagnostic: bench the product build and the occupancy / ablation variants (config B) under
-# rocprofv3 kernel tracing, so every variant's kernel durations come from the profiler.
+# Diagnostic: bench the product build and diagnostic variants (config B) under rocprofv3 kernel
+# tracing, so every variant's kernel durations come from the profiler.
+#   tools/variants_run.sh [label=ENV=VALUE ...]   (default: ablation + grid variants)
 set -e
 run() {  # label, then env assignments for the variant
   local label=$1; shift
@@ -9,5 +10,11 @@ run() {  # label, then env assignments for the variant
 }
 run default UPE_BENCH_EVENTS=1
 run noev UPE_BENCH_EVENTS=0
-for t in 512 1024; do run t$t UPE_GPU_LIB_DIAG=$PWD/build/occ/libupe_gpu_t$t.so; done
-for a in 1 2 4 8 15 16 64; do run a$a UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a$a.so; done
+if [ $# -eq 0 ]; then
+  set -- a2=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a2.so \
+         a4=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a4.so \
+         a15=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a15.so \
+         a64=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a64.so \
+         g4=UPE_GPU_BLOCKS_PER_CU=4 g16=UPE_GPU_BLOCKS_PER_CU=16
+fi
+for spec in "$@"; do run "${spec%%=*}" "${spec#*=}"; done

@@ -11,23 +11,32 @@
 //
 // Data layout (DESIGN.md "HBM layout"): frames packed back to back at 16-byte aligned starts,
 // one uint64 descriptor per packet (offset << 16 | len), one uint32 verdict per packet.  A lane
-// reads at most the first UPE_HDR_WINDOW bytes of its frame as 16-byte vector loads (48 bytes for
-// an option-less IPv4 header).  The rule table is compiled into structure-of-arrays streams that
-// a wave scans with wave-uniform (scalar-unit) loads, so rule operands arrive in SGPRs; the
-// per-rule work is a few VALU xor/and-or against them, with an early exit as soon as every lane
-// of the wave has its first match (ballot).
+// loads the first 80 bytes of its frame as five 16-byte vector loads, issued together (the batch
+// buffer carries a 96-byte tail, so the last frame's window is readable); frames are 16-byte
+// aligned, so the loads never split a frame's line between two requests more than necessary.
 //
-// Two launches per batch.  classify runs one 256-packet tile per workgroup and keeps the tile's
-// counters, rule_stats histogram (LDS) and L1 bookkeeping on chip, flushing them with device
-// atomics into replicated per-batch accumulators (replica = tile % 32, so no address sees more
-// than a few dozen adders).  finalize folds the accumulators into the worker totals and updates
-// the L1 state.  The accumulators are double-buffered by batch parity, so finalize only reads.
+// Fast path: option-less IPv4 (first byte 0x45, len >= 34) and IPv6 (len >= 54), which covers
+// every well-formed packet of the benchmark configurations, is parsed branch-free from those
+// registers; everything else (ARP, IPv4 options, truncated or foreign frames) takes the general
+// path, entered only by waves that hold such a packet.
+//
+// The rule table is compiled into structure-of-arrays streams that a wave scans with
+// wave-uniform (scalar-unit) loads, so rule operands arrive in SGPRs; the per-rule work is a few
+// VALU xor / and-or against them, with an early exit as soon as every lane of the wave has its
+// first match (ballot).
+//
+// One launch per batch, persistent workgroups: the grid is what the chip holds at once and
+// workgroup b takes 256-packet tiles b, b + grid, ...  A workgroup keeps its tiles' counters,
+// rule_stats histogram (LDS) and L1 bookkeeping on chip and flushes them once, with device
+// atomics, into replicated per-batch accumulators (replica = workgroup % 32), then takes an
+// arrival ticket.  The workgroup that arrives last folds the accumulators into the worker
+// totals, updates the L1 state and re-arms everything for the next batch.
 //
 // Neighbour lookups answer arp_get_mac / ndp_get_mac exactly without walking the reference's
 // linear-probe chains: at upload the host keeps only the entries a reference probe can reach
-// (probe from the home slot, first valid match before the first invalid slot) and re-hashes
-// them into a half-empty multiplicative-hash table; every answer equals the reference's for the
-// snapshot and a lookup costs ~1-2 probes.
+// (probe from the home slot, first valid match before the first invalid slot) and places them
+// by two-choice cuckoo hashing; every answer equals the reference's for the snapshot and a
+// lookup is one round trip (both candidate slots loaded at once).
 //
 // The worker's one-entry L1 neighbour caches are sequential state (src/worker.c:186-195,
 // 218-225), emulated exactly.  If the starting L1 entry agrees with the
@@ -35,12 +44,14 @@
 // is the final L1 entry: the last table hit, if any packet missed the starting entry and hit the
 // table.  If it disagrees (after a table change, or the calloc'd NDP entry for ::), a packet
 // whose destination equals the starting entry takes the entry's MAC iff no earlier packet missed
-// the entry and hit the table: classify flags the tiles that hold such packets and finalize,
-// which knows the batch's first miss-then-hit index, rewrites them after the kernel boundary.
+// the entry and hit the table: a workgroup holding such packets flags their tiles and releases
+// its stores, and the last workgroup, which knows the batch's first miss-then-hit index,
+// rewrites them.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <array>
@@ -62,22 +73,25 @@ constexpr int kTile = kBlock;
 #define UPE_WAVES_PER_SIMD 8
 #endif
 constexpr int kWavesPerSimd = UPE_WAVES_PER_SIMD;   // 8 -> VGPR budget 64
-constexpr int kUnroll = 4;             // rules per early-exit check
+constexpr int kUnroll = 4;             // rules per early-exit check (rule table padding unit)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kLdsStatsMax = 4096;     // rule_stats histogrammed in LDS up to this many rules
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
+constexpr int kShards = 8;             // arrival-ticket shards
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
-// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 16 empty finalize, 32 no finalize
-// launch, 64 empty classify
+// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify
 constexpr unsigned kAblate = UPE_ABLATE;
+// s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt not waited (gfx9 encoding)
+constexpr int kWaitVm0 = 0x0F70;
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
 // rv4[i]: header + first address word, used for every packet:
 //   x0 = ip_ver | proto << 8 | src_port << 16 and its wildcard mask m0
-//   x1 = dst_port and mask m1
+//   x1 = dst_port and mask m1; m1 bit 31 (x1 bit 31 clear, so it never decides a match) marks a
+//   rule with IPv6 address words, the only rules an IPv6 key must test against rv6
 //   s0/sm0, d0/dm0: union bytes 0-3 of src/dst as LE u32 (the v4 view, rule_t.src_ip.v4),
 //   pre-masked so a match is ((key ^ x) & m) == 0 for every pair.
 // rv6[i]: union words 1-3 of src/dst (pre-masked) and masks, used only by IPv6 packets.
@@ -85,13 +99,14 @@ constexpr unsigned kAblate = UPE_ABLATE;
 struct __attribute__((aligned(16))) RuleV4 {
     uint32_t x0, m0, x1, m1, s0, sm0, d0, dm0;
 };
+constexpr uint32_t kRuleV6Words = 0x80000000u;
 struct __attribute__((aligned(16))) RuleV6 {
     uint32_t s[3], sm[3], d[3], dm[3], pad[4];
 };
 
 // L1 state in word form (device resident between batches) + whether each entry agrees with the
-// current neighbour snapshot (maintained by the last workgroup of every batch and by
-// upe_refresh after every table / L1 upload).
+// current neighbour snapshot (maintained by every batch's last workgroup and by upe_refresh
+// after every table / L1 upload).
 struct DevL1 {
     uint32_t arp_ip, arp_mac_lo, arp_mac_hi;
     uint32_t ndp_ip[4];
@@ -100,30 +115,35 @@ struct DevL1 {
     uint32_t pad[5];
 };
 
-// Per-batch accumulators, double-buffered by batch parity: classify(e) adds into acc[e & 1] with
-// device atomics and clears acc[(e + 1) & 1] for the next batch; finalize(e) only reads acc[e & 1],
-// so any number of finalize workgroups can read it without a re-arm race.
+// Per-batch accumulators.  Every workgroup adds its totals with device atomics into replica
+// (workgroup % kReps); the batch's last workgroup reads them back with atomic exchanges, which
+// also re-arm them for the next batch.
 enum { C_PARSED, C_MATCHED, C_FWD, C_DROPPED, C_CONSUMED, C_ARP_LEARN, C_ARP_REPLY, C_CTRL,
-       C_CAND, C_N };   // C_CAND: tiles holding packets a disagreeing starting entry may answer
+       C_CAND, C_N };   // C_CAND: workgroups holding packets a disagreeing start entry may answer
 enum { M_F4, M_F6, M_CTRL, M_N };  // minima: first miss-then-hit per family, first control packet
 enum { X_M4, X_M6, X_N };          // maxima: last table hit per family (index + 1, 0 = none)
+constexpr int kAccFields = C_N + M_N + X_N;
 struct BatchAcc {
     uint32_t cnt[kReps][C_N];
     uint32_t mins[kReps][M_N];
     uint32_t maxs[kReps][X_N];
-    // the starting L1 entries' MACs and whether each disagreed with the table (copied by
-    // classify, read by finalize, which itself rewrites the live L1 state)
-    uint32_t start_arp_lo, start_arp_hi, start_ndp_lo, start_ndp_hi, look4, look6, pad[2];
 };
-// Payload of the last table hit of a 64-packet chunk (one wave's share of a tile), written by the
-// lane that holds it; finalize reads the one chunk the batch maximum points at.
-struct __attribute__((aligned(16))) ChunkPay {
-    uint32_t m4_dst, m4_mac_lo, m4_mac_hi, pad0;
-    uint32_t m6_dst[4];
-    uint32_t m6_mac_lo, m6_mac_hi, pad1[2];
+// Payload of a workgroup's last table hit per family; the last workgroup reads the one the batch
+// maximum points at.  Written with agent-scope (sc1) stores before the arrival ticket.
+struct __attribute__((aligned(64))) TilePay {
+    uint32_t m4_dst, m4_mac_lo, m4_mac_hi;
+    uint32_t m6_dst[4], m6_mac_lo, m6_mac_hi;
+    uint32_t pad[7];
+};
+constexpr int kPayWords = 9;
+// Arrival tickets: shard s counts the workgroups b with b % kShards == s (one 128-byte line
+// each); a shard's last arrival bumps `top`, and the workgroup that completes `top` is last.
+struct Tickets {
+    uint32_t shard[kShards][32];
+    uint32_t top[32];
 };
 
-// Accumulated worker state (device resident).
+// Accumulated worker state.
 struct DevTotals {
     unsigned long long cnt[8];     // upe_counters_t order
     unsigned long long n_ctrl, first_ctrl;
@@ -131,6 +151,24 @@ struct DevTotals {
     unsigned long long error;
 };
 
+// Everything a batch reads or writes besides the packets and the tables, in one device
+// allocation reached through one kernel argument (keeps the kernel's scalar registers free).
+struct DevState {
+    DevL1 l1;
+    DevTotals totals;
+    BatchAcc acc;
+    Tickets tickets;
+    unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
+    TilePay* pay;                    // [grid]
+    uint32_t* cand_tile;             // [ntiles], zero between batches
+    unsigned long long* stats;       // [cap][2] worker rule_stats (mid-size and large tables)
+    unsigned long long* stats_idx;   // [nrules_pad][2] totals per sorted index (small tables)
+};
+
+// Neighbour index (built by upe_gpu_load_neigh): the entries a reference probe reaches, placed
+// by two-choice cuckoo hashing, so that every key sits in one of its two candidate slots.
+//   ARP slot: uint4 {ip, mac0..3, mac4..5 | used << 16, 0}
+//   NDP slot: 2 x uint4 {ip words 0..3}, {mac0..3, mac4..5 | used << 16, 0, 0}
 struct NeighIndex {
     const uint4* t;
     uint32_t bits;   // log2(slots); 0 = empty
@@ -143,21 +181,13 @@ struct Args {
     uint32_t* verdict;
     uint32_t n;
     uint32_t ntiles;
-    uint32_t parity;               // batch sequence number & 1
     const RuleV4* rv4;
     const RuleV6* rv6;
     const int2* rinfo;
     uint32_t nrules_pad;           // multiple of kUnroll, padding rules never match
-    NeighIndex arp, ndp;           // reachable-entry indexes (two-choice cuckoo)
-    DevL1* l1;
-    BatchAcc* acc;                 // [2]
-    ChunkPay* pay;                 // [ntiles * kWaves]
-    uint32_t* cand_tile;           // [ntiles] families with packets the starting entry may answer
-    unsigned long long* acc_stats; // [2][kReps][nrules_pad][2] when nrules_pad <= kSmallRules
-    unsigned long long* stats;     // [cap][2] worker totals (rule_stat_t), large tables
-    unsigned long long* stats_idx; // [nrules_pad][2] totals per sorted index, small tables
-    DevTotals* totals;
     uint32_t port_mac_lo, port_mac_hi, port_ip4;
+    NeighIndex arp, ndp;
+    DevState* st;
 };
 
 // ---- small helpers ------------------------------------------------------------------------
@@ -174,12 +204,19 @@ __device__ __forceinline__ uint32_t len_mask(uint32_t len, int j) {
 __device__ __forceinline__ uint32_t be16_lo(uint32_t x) {             // BE u16 in bytes 0,1
     return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu);
 }
-// Neighbour index (built by upe_gpu_load_neigh): the entries a reference probe reaches, placed
-// by two-choice cuckoo hashing, so that every key sits in one of its two candidate slots.  A
-// lookup loads both slots at once: one memory round trip for every packet, no probe loop (a
-// linear-probe walk costs the longest chain of the wave, one dependent load per step).
-//   ARP slot: uint4 {ip, mac0..3, mac4..5 | used << 16, 0}
-//   NDP slot: 2 x uint4 {ip words 0..3}, {mac0..3, mac4..5 | used << 16, 0, 0}
+// RFC 1071 fold of a sum of native-LE u16 words held as a sum of u32 (u32 = lo + hi * 2^16,
+// and 2^16 == 1 in one's-complement arithmetic), complemented: src/parser.c:137-169.
+__device__ __forceinline__ uint32_t csum_fold(unsigned long long sum) {
+    uint32_t f = (uint32_t)(sum & 0xFFFFFFFFull) + (uint32_t)(sum >> 32);
+    f += (uint32_t)(sum & 0xFFFFFFFFull) > f ? 1u : 0u;            // end-around carry
+    f = (f & 0xFFFFu) + (f >> 16);
+    f = (f & 0xFFFFu) + (f >> 16);
+    f = (f & 0xFFFFu) + (f >> 16);
+    return (~f) & 0xFFFFu;
+}
+__device__ __forceinline__ void store16(uint4* p, uint4 v) { *p = v; }
+
+// ---- neighbour lookups ----------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t fold_v6(const uint32_t ip[4]) {
     return (ip[0] * 0x9E3779B1u) ^ (ip[1] * 0x85EBCA77u) ^ (ip[2] * 0xC2B2AE3Du) ^
            (ip[3] * 0x27D4EB2Fu);
@@ -237,27 +274,43 @@ __global__ void upe_refresh(DevL1* l1, NeighIndex arp, NeighIndex ndp) {
     if (threadIdx.x == 0 && blockIdx.x == 0) refresh_ok(l1, arp, ndp);
 }
 
+// Rule words are read through the constant address space: the compiler may then use scalar
+// (s_load) loads, which it will not do through a generic pointer it cannot prove unwritten.
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+template <typename V, typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) V* as_const(const T* p) {
+    return (const __attribute__((address_space(4))) V*)p;
+}
+
 // First-match scan (reference src/rule_table.c:163-176 over match_rule :76-91).  Every lane of
 // the wave walks the same rules in sorted order; rule words are wave-uniform loads.  `done`
-// lanes (already matched, or not scanning) are ignored.  V6 = some lane holds an IPv6 key.
+// lanes (already matched, or not scanning) are ignored.  V6 = some lane holds an IPv6 key; rules
+// without IPv6 address words skip the rv6 test (a scalar branch).
 template <bool V6>
 __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4],
                                                const uint32_t d[4]) {
     uint32_t hit = kNone;
-    const uint32_t m6 = is6 ? 0xFFFFFFFFu : 0u;
-    for (uint32_t base = 0; base < a.nrules_pad; base += kUnroll) {
+    static_assert(sizeof(RuleV4) == 32 && sizeof(RuleV6) == 64, "rule stream strides");
+    const auto* rv4 = as_const<u32x8>(a.rv4);
+    const auto* rv6 = as_const<u32x16>(a.rv6);
+    for (uint32_t b = 0; b < a.nrules_pad; b += kUnroll) {
+        // the rule index is wave-uniform: say so, so rule words come through the scalar unit
+        const uint32_t base = __builtin_amdgcn_readfirstlane(b);
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const RuleV4 r = a.rv4[base + u];
-            uint32_t x = ((k0 ^ r.x0) & r.m0) | ((k1 ^ r.x1) & r.m1) | ((s[0] ^ r.s0) & r.sm0) |
-                         ((d[0] ^ r.d0) & r.dm0);
-            if (V6) {
-                const RuleV6 q = a.rv6[base + u];
-                uint32_t y = ((s[1] ^ q.s[0]) & q.sm[0]) | ((s[2] ^ q.s[1]) & q.sm[1]) |
-                             ((s[3] ^ q.s[2]) & q.sm[2]) | ((d[1] ^ q.d[0]) & q.dm[0]) |
-                             ((d[2] ^ q.d[1]) & q.dm[1]) | ((d[3] ^ q.d[2]) & q.dm[2]);
-                x |= y & m6;
+            // RuleV4 words: x0 m0 x1 m1 s0 sm0 d0 dm0
+            const u32x8 r = rv4[base + u];
+            uint32_t x = ((k0 ^ r[0]) & r[1]) | ((k1 ^ r[2]) & r[3]) | ((s[0] ^ r[4]) & r[5]) |
+                         ((d[0] ^ r[6]) & r[7]);
+            if (V6 && (r[3] & kRuleV6Words)) {
+                // RuleV6 words: s[3] sm[3] d[3] dm[3]
+                const u32x16 q = rv6[base + u];
+                const uint32_t y = ((s[1] ^ q[0]) & q[3]) | ((s[2] ^ q[1]) & q[4]) |
+                                   ((s[3] ^ q[2]) & q[5]) | ((d[1] ^ q[6]) & q[9]) |
+                                   ((d[2] ^ q[7]) & q[10]) | ((d[3] ^ q[8]) & q[11]);
+                if (is6) x |= y;
             }
             if (!done && x == 0) {
                 hit = base + u;
@@ -270,266 +323,415 @@ __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is
 }
 
 // ------------------------------------------------------------------------------------------
-// classify: one 256-packet tile per workgroup
+// General path: every live packet the fast path does not cover (ARP and NDP control frames,
+// IPv4 with options, truncated, foreign or malformed frames).  Same outputs as the fast path.
+// ------------------------------------------------------------------------------------------
+struct Parsed {
+    bool ok, consumed, v6;
+    uint32_t flags;                // UPE_VF_ARP_LEARN / UPE_VF_ARP_REPLY
+    uint32_t proto, sport, dport;
+    uint32_t s[4], d[4];
+    uint32_t ttl, c1w1, c1w2;      // TTL / hop, and bytes 20..27 as they are forwarded
+};
+
+// Out of line: only waves holding such a packet pay for its registers and code.
+struct Port {
+    uint32_t mac_lo, mac_hi, ip4;
+};
+__device__ __noinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r) {
+    r.ok = false; r.consumed = false; r.v6 = false; r.flags = 0;
+    r.proto = r.sport = r.dport = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.s[j] = r.d[j] = 0;
+    r.ttl = 0;
+    // its own copy of the window (the frame is in cache): bytes 0..95, IPv4 options reach 94
+    uint32_t w[24];
+    {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const uint4 v = q[c];
+            w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+        }
+    }
+    r.c1w1 = w[5];
+    r.c1w2 = w[6];
+    // Bytes 12/13 as a zero-filled pktbuf would hold them (the ethertype is read before any
+    // length gate, src/worker.c:24-25).
+    const uint32_t b12 = len > 12 ? byte_of(w[3], 0) : 0u;
+    const uint32_t b13 = len > 13 ? byte_of(w[3], 1) : 0u;
+    const uint32_t et = (b12 << 8) | b13;
+    const bool is_v4 = et == 0x0800u;
+    const bool is_v6 = et == 0x86DDu;
+    const uint32_t ihl = byte_of(w[3], 2) & 0xFu;
+    r.v6 = is_v6;
+
+    // ---- handle_control_packet, reference src/worker.c:23-104 ----
+    if (et == 0x0806u) {
+        // The ARP header (bytes 14..41) is read without a length check: bytes at or past len
+        // read as zero, as in a zero-filled pktbuf.
+        uint32_t z[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) z[j] = w[j] & len_mask(len, j);
+        const bool wellformed = (z[3] >> 16) == 0x0100u && z[4] == 0x04060008u;
+        if (wellformed) {
+            r.flags |= UPE_VF_ARP_LEARN;
+            const bool request = (z[5] & 0xFFFFu) == 0x0100u;
+            const uint32_t tpa = bswap32(at2(z[10], z[9]));
+            if (request && a.ip4 != 0 && tpa == a.ip4) {
+                // In-place reply, src/worker.c:42-51, assembled a dword at a time.
+                uint32_t nw[12];
+                nw[0] = at2(z[2], z[1]);                                  // eth.dst = eth.src
+                nw[1] = (z[2] >> 16) | (a.mac_lo << 16);                  // eth.src = port MAC
+                nw[2] = (a.mac_lo >> 16) | (a.mac_hi << 16);
+                nw[3] = z[3];
+                nw[4] = z[4];
+                nw[5] = 0x0200u | (a.mac_lo << 16);                       // op = REPLY, sha
+                nw[6] = (a.mac_lo >> 16) | (a.mac_hi << 16);
+                nw[7] = bswap32(a.ip4);                                   // spa = port IPv4
+                nw[8] = at2(z[6], z[5]);                                  // tha = old sha
+                nw[9] = (z[6] >> 16) | (z[7] << 16);                      // tpa = old spa
+                nw[10] = (z[7] >> 16) | (z[10] & 0xFFFF0000u);
+                nw[11] = z[11];
+                // bytes at or past len keep the buffer's own (never transmitted) bytes
+#pragma unroll
+                for (int j = 0; j < 12; ++j) {
+                    const uint32_t m = len_mask(len, j);
+                    w[j] = (nw[j] & m) | (w[j] & ~m);
+                }
+                if (!(kAblate & 8)) {
+                    uint4* q = reinterpret_cast<uint4*>(p);
+                    store16(&q[0], make_uint4(w[0], w[1], w[2], w[3]));
+                    store16(&q[1], make_uint4(w[4], w[5], w[6], w[7]));
+                    store16(&q[2], make_uint4(w[8], w[9], w[10], w[11]));
+                }
+                r.flags |= UPE_VF_ARP_REPLY;
+            }
+        }
+    }
+    if (is_v6 && len >= 78u && byte_of(w[5], 0) == 58u) {               // src/worker.c:58-100
+        const uint32_t type = byte_of(w[13], 2);                        // byte 54
+        if (type == 135u || type == 136u) r.consumed = true;
+    }
+
+    // ---- parse_flow_key, reference src/parser.c:6-111 ----
+    if (!r.consumed && len >= 14u) {
+        if (is_v4) {
+            const uint32_t ver = byte_of(w[3], 2) >> 4;
+            const uint32_t hl = ihl * 4;
+            if (len - 14 >= 20u && ver == 4 && hl >= 20 && len - 14 >= hl) {
+                r.proto = byte_of(w[5], 3);                                  // byte 23
+                r.s[0] = bswap32(at2(w[7], w[6]));                           // bytes 26..29
+                r.d[0] = bswap32(at2(w[8], w[7]));                           // bytes 30..33
+                const uint32_t l4len = len - 14 - hl;
+                // L4 starts at byte 14 + 4 * ihl = 4 * (ihl + 3) + 2 (registers are not
+                // indexable: select the window by IHL)
+                uint32_t l4w0 = 0, l4w1 = 0, l4w3 = 0;
+#pragma unroll
+                for (int h = 5; h <= 15; ++h) {
+                    if ((int)ihl == h) {
+                        l4w0 = at2(w[h + 4], w[h + 3]);
+                        l4w1 = at2(w[h + 5], w[h + 4]);
+                        l4w3 = at2(w[h + 7], w[h + 6]);
+                    }
+                }
+                if (r.proto == 17u) {
+                    r.ok = l4len >= 8u;
+                    r.sport = be16_lo(l4w0);
+                    r.dport = be16_lo(l4w0 >> 16);
+                } else if (r.proto == 6u) {
+                    const uint32_t thl = (byte_of(l4w3, 0) >> 4) * 4;
+                    r.ok = l4len >= 20u && thl >= 20u && l4len >= thl;
+                    r.sport = be16_lo(l4w0);
+                    r.dport = be16_lo(l4w0 >> 16);
+                } else if (r.proto == 1u) {
+                    r.ok = l4len >= 8u;
+                    r.sport = be16_lo(l4w1);                                 // icmp id
+                    r.dport = be16_lo(l4w0);                                 // type << 8 | code
+                }
+                // checksum over IHL*4 bytes with the TTL decremented and the field zeroed:
+                // sum of u16 words = (w3 >> 16) + w4 + ... + w[2 + ihl] + (w[3 + ihl] & 0xFFFF)
+                r.ttl = byte_of(w[5], 2);
+                const uint32_t w5n = (w[5] & 0xFF00FFFFu) | (((r.ttl - 1) & 0xFFu) << 16);
+                const uint32_t w6z = w[6] & 0xFFFF0000u;
+                unsigned long long sum = (w[3] >> 16) + (unsigned long long)w[4] + w5n + w6z;
+#pragma unroll
+                for (int k = 7; k <= 17; ++k)
+                    if ((uint32_t)k <= 2 + ihl) sum += w[k];
+#pragma unroll
+                for (int h = 5; h <= 15; ++h)
+                    if ((int)ihl == h) sum += w[3 + h] & 0xFFFFu;
+                r.c1w1 = w5n;
+                r.c1w2 = w6z | csum_fold(sum);
+            }
+        } else if (is_v6 && len - 14 >= 40u) {
+            // (len >= 54: only a fast-path packet; reached here when len < 54 -> parse fails)
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// The batch's last workgroup (wave 0, every other workgroup has arrived): fold the accumulators
+// into the worker totals, update the L1 state, give the starting L1 entry's answer to the
+// packets it answered in the reference, and re-arm accumulators and tickets for the next batch.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void batch_tail(const Args& a, int lane, bool look4, bool look6) {
+    __shared__ unsigned long long t_cnt[C_N];
+    __shared__ uint32_t t_min[M_N], t_max[X_N];
+    __shared__ unsigned long long t_st[2 * kSmallRules];
+    DevState* S = a.st;
+    const bool small = a.nrules_pad <= (uint32_t)kSmallRules;
+    const uint32_t E = 2 * a.nrules_pad;
+    if (lane < C_N) t_cnt[lane] = 0;
+    if (lane < M_N) t_min[lane] = kNone;
+    if (lane < X_N) t_max[lane] = 0;
+    for (uint32_t e = lane; e < 2 * kSmallRules; e += 64) t_st[e] = 0;
+    __builtin_amdgcn_wave_barrier();
+
+    // accumulators: read and re-arm in one atomic exchange per word (reads the value every
+    // workgroup's atomics left, whichever XCD they ran on)
+    uint32_t* accw = reinterpret_cast<uint32_t*>(&S->acc);
+    constexpr uint32_t kCntW = kReps * C_N, kMinW = kReps * M_N, kAccW = kReps * kAccFields;
+    for (uint32_t k = lane; k < kAccW; k += 64) {
+        const bool is_min = k >= kCntW && k < kCntW + kMinW;
+        const uint32_t v = __hip_atomic_exchange(&accw[k], is_min ? kNone : 0u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        if (k < kCntW) {
+            if (v) atomicAdd(&t_cnt[k % C_N], (unsigned long long)v);
+        } else if (is_min) {
+            atomicMin(&t_min[(k - kCntW) % M_N], v);
+        } else {
+            atomicMax(&t_max[(k - kCntW - kMinW) % X_N], v);
+        }
+    }
+    if (small) {
+        for (uint32_t k = lane; k < E * kReps; k += 64) {
+            const unsigned long long v = __hip_atomic_exchange(
+                &S->acc_stats[k / E][k % E], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v) atomicAdd(&t_st[k % E], v);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // LDS results visible to the wave
+
+    // worker totals and this batch's summary
+    if (small && (uint32_t)lane < E && t_st[lane]) atomicAdd(&S->stats_idx[lane], t_st[lane]);
+    if (small && (uint32_t)lane + 64 < E && t_st[lane + 64])
+        atomicAdd(&S->stats_idx[lane + 64], t_st[lane + 64]);
+    DevTotals* T = &S->totals;
+    if (lane < 8) {
+        // upe_counters_t order: pkts_in, then C_PARSED .. C_ARP_REPLY
+        const unsigned long long b = lane == 0 ? (unsigned long long)a.n : t_cnt[lane - 1];
+        if (b) atomicAdd(&T->cnt[lane], b);
+        T->batch[lane] = b;
+    }
+    if (lane == 8) T->n_ctrl = t_cnt[C_CTRL];
+    if (lane == 9)
+        T->first_ctrl = t_min[M_CTRL] == kNone ? ~0ull : (unsigned long long)t_min[M_CTRL];
+
+    // Packets whose destination is the starting entry, before the first miss-then-hit packet of
+    // their family, took the entry's MAC (found) in the reference: src/worker.c:186-188, 218-220.
+    // Only flagged tiles are visited (their workgroups released their stores).
+    DevL1* L = &S->l1;
+    if ((look4 || look6) && t_cnt[C_CAND] != 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t f[2] = {t_min[M_F4], t_min[M_F6]};
+        const uint32_t lo[2] = {L->arp_mac_lo, L->ndp_mac_lo};
+        const uint32_t hi[2] = {L->arp_mac_hi, L->ndp_mac_hi};
+        // nothing at or after the later of the two first-hit indexes needs the start entry
+        const uint32_t fmax = max(look4 ? f[0] : 0u, look6 ? f[1] : 0u);
+        const uint32_t tend = fmax == kNone ? a.ntiles : min(a.ntiles, fmax / kTile + 1);
+        for (uint32_t base = 0; base < tend; base += 64) {
+            const uint32_t t = base + (uint32_t)lane;
+            // flags were set with device atomics: read and re-arm them the same way
+            const uint32_t cbt = t < tend ? __hip_atomic_exchange(&S->cand_tile[t], 0u,
+                                                                  __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0u;
+            unsigned long long pend = __ballot(cbt != 0);
+            while (pend) {
+                const int l = __ffsll((long long)pend) - 1;
+                pend &= pend - 1;
+                const uint32_t tt = base + (uint32_t)l;
+                const uint32_t fam_ok = (uint32_t)__shfl((int)cbt, l, 64);
+                for (uint32_t q = 0; q < (uint32_t)kTile; q += 64) {
+                    const uint32_t i = tt * kTile + q + (uint32_t)lane;
+                    if (i >= a.n) continue;
+                    const uint32_t v = a.verdict[i];
+                    if ((v & 0xFu) != UPE_V_FWD || !(v & UPE_VF_L1_INIT)) continue;
+                    uint8_t* p = a.frames + (a.desc[i] >> 16);
+                    const int fam = (p[12] == 0x86 && p[13] == 0xDD) ? 1 : 0;
+                    if (!((fam_ok >> fam) & 1u) || i >= f[fam]) continue;
+                    uint32_t* w = reinterpret_cast<uint32_t*>(p);
+                    w[0] = lo[fam];
+                    w[1] = hi[fam] | (a.port_mac_lo << 16);
+                    w[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
+                    a.verdict[i] = v | UPE_VF_NEIGH_HIT;
+                }
+            }
+        }
+        // flagged tiles past tend keep their flag: clear them too
+        for (uint32_t t = tend + (uint32_t)lane; t < a.ntiles; t += 64)
+            __hip_atomic_store(&S->cand_tile[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // New L1 state: the last table hit, if some packet missed the starting entry and hit the
+    // table (from then on the cache only ever holds table answers, so it agrees with the
+    // table); otherwise unchanged.
+    if (lane == 0 && t_min[M_F4] != kNone && t_max[X_M4] != 0) {
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(
+            &S->pay[((t_max[X_M4] - 1) / kTile) % gridDim.x]);
+        uint32_t v[3];
+        for (int j = 0; j < 3; ++j)
+            v[j] = __hip_atomic_load(P + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L->arp_ip = v[0];
+        L->arp_mac_lo = v[1];
+        L->arp_mac_hi = v[2];
+        L->arp_ok = 1;
+    }
+    if (lane == 1 && t_min[M_F6] != kNone && t_max[X_M6] != 0) {
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(
+            &S->pay[((t_max[X_M6] - 1) / kTile) % gridDim.x]);
+        uint32_t v[6];
+        for (int j = 0; j < 6; ++j)
+            v[j] = __hip_atomic_load(P + 3 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < 4; ++j) L->ndp_ip[j] = v[j];
+        L->ndp_mac_lo = v[4];
+        L->ndp_mac_hi = v[5];
+        L->ndp_ok = 1;
+    }
+    // re-arm the arrival tickets
+    if (lane < kShards)
+        __hip_atomic_store(&S->tickets.shard[lane][0], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == kShards)
+        __hip_atomic_store(&S->tickets.top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// classify: persistent workgroups over 256-packet tiles
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     __shared__ uint32_t s_cnt[C_N];
     __shared__ uint32_t s_red[kWaves][8];
+    __shared__ uint32_t s_pay[kWaves][kPayWords];
+    __shared__ uint32_t s_l1[8];   // starting L1 entries: arp ip, ndp ip[4], look flags
 
     if (kAblate & 64) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t rep = tile % kReps;
     const bool lds_stats = a.nrules_pad <= (uint32_t)kLdsStatsMax;
     const bool small_stats = a.nrules_pad <= (uint32_t)kSmallRules;
-    BatchAcc* A = &a.acc[a.parity];
 
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
     if (tid < C_N) s_cnt[tid] = 0;
-
-    // L1 state at batch start (uniform).
-    const DevL1* l1 = a.l1;
-    const uint32_t l1_arp_ip = l1->arp_ip;
-    uint32_t l1_ndp[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) l1_ndp[j] = l1->ndp_ip[j];
-    const bool look4 = !l1->arp_ok;
-    const bool look6 = !l1->ndp_ok;
-
-    if (tile == 0) {
-        // clear the other parity's accumulators for the next batch; record the starting
-        // entries for this batch's finalize
-        BatchAcc* N = &a.acc[a.parity ^ 1];
-        uint32_t* nw = reinterpret_cast<uint32_t*>(N);
-        for (uint32_t k = tid; k < sizeof(BatchAcc) / 4; k += kBlock) {
-            const uint32_t off = k * 4;
-            const bool is_min = off >= offsetof(BatchAcc, mins) && off < offsetof(BatchAcc, maxs);
-            nw[k] = is_min ? kNone : 0u;
-        }
-        if (small_stats) {
-            unsigned long long* ns = a.acc_stats + (size_t)(a.parity ^ 1) * kReps * 2 * a.nrules_pad;
-            for (uint32_t k = tid; k < kReps * 2 * a.nrules_pad; k += kBlock) ns[k] = 0;
-        }
-        if (tid == 0) {
-            A->start_arp_lo = l1->arp_mac_lo;
-            A->start_arp_hi = l1->arp_mac_hi;
-            A->start_ndp_lo = l1->ndp_mac_lo;
-            A->start_ndp_hi = l1->ndp_mac_hi;
-            A->look4 = look4;
-            A->look6 = look6;
-        }
+    if (tid < 8) {
+        const DevL1* l1 = &a.st->l1;
+        const uint32_t v[8] = {l1->arp_ip, l1->ndp_ip[0], l1->ndp_ip[1], l1->ndp_ip[2],
+                               l1->ndp_ip[3], (l1->arp_ok ? 0u : 1u) | (l1->ndp_ok ? 0u : 2u),
+                               0u, 0u};
+        s_l1[tid] = v[tid];
     }
     __syncthreads();
+    const uint32_t look = s_l1[5];   // bit 0: the ARP entry disagrees with the table, bit 1: NDP
+    const bool look4 = look & 1u, look6 = look & 2u;
 
-    {
+    // per-wave L1 bookkeeping over this workgroup's tiles (wave-uniform)
+    uint32_t wf4 = kNone, wf6 = kNone, wfc = kNone, wm4 = 0, wm6 = 0, wcb = 0;
+    // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
+    // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
+    // workgroup, at the very end of its life, not once per tile.
+    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint32_t i = tile * kTile + (uint32_t)tid;
         const bool live = i < a.n;
         const uint64_t dsc = live ? a.desc[i] : 0;
         const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
-        uint8_t* p = a.frames + (dsc >> 16);
+        // frames are 16-byte aligned: the offset in 16-byte units fits one register
+        const uint32_t off16 = (uint32_t)(dsc >> 20);
+        uint8_t* p = a.frames + ((size_t)off16 << 4);
 
-        // ---- header window: chunks 0-2 (bytes 0..47) for every live lane ----
-        uint32_t w[24];
+        // ---- header window: bytes 0..79, five 16-byte loads issued together ----
+        uint32_t w[20];
 #pragma unroll
-        for (int j = 0; j < 24; ++j) w[j] = 0;
+        for (int j = 0; j < 20; ++j) w[j] = 0;
         if (live) {
             const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const uint4 v = q[c];
-                w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-            }
-        }
-        // Bytes 12/13 as a zero-filled pktbuf would hold them (the ethertype is read before
-        // any length gate, src/worker.c:24-25).
-        const uint32_t b12 = len > 12 ? byte_of(w[3], 0) : 0u;
-        const uint32_t b13 = len > 13 ? byte_of(w[3], 1) : 0u;
-        const uint32_t et = (b12 << 8) | b13;
-        const bool is_v4 = et == 0x0800u;
-        const bool is_v6 = et == 0x86DDu;
-        const uint32_t ihl = byte_of(w[3], 2) & 0xFu;
-        // chunks 3-5 only for IPv6 and IPv4 with options
-        if (live && (is_v6 || (is_v4 && ihl > 5))) {
-            const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-            for (int c = 3; c < 6; ++c) {
+            for (int c = 0; c < 5; ++c) {
                 const uint4 v = q[c];
                 w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
             }
         }
 
-        uint32_t flags = 0;
-        bool consumed = false;
-        bool wrote0 = false;  // chunk 0 (bytes 0..15) modified
-        bool wrote1 = false;  // chunk 1
-
-        // ---- handle_control_packet, reference src/worker.c:23-104 ----
-        if (live && et == 0x0806u) {
-            // The ARP header (bytes 14..41) is read without a length check: bytes at or past
-            // len read as zero, as in a zero-filled pktbuf.
-            uint32_t z[12];
-#pragma unroll
-            for (int j = 0; j < 12; ++j) z[j] = w[j] & len_mask(len, j);
-            const bool wellformed = (z[3] >> 16) == 0x0100u && z[4] == 0x04060008u;
-            if (wellformed) {
-                flags |= UPE_VF_ARP_LEARN;
-                const bool request = (z[5] & 0xFFFFu) == 0x0100u;
-                const uint32_t tpa = bswap32(at2(z[10], z[9]));
-                if (request && a.port_ip4 != 0 && tpa == a.port_ip4) {
-                    // In-place reply, src/worker.c:42-51, assembled a dword at a time.
-                    uint32_t nw[12];
-                    nw[0] = at2(z[2], z[1]);                                  // eth.dst = eth.src
-                    nw[1] = (z[2] >> 16) | (a.port_mac_lo << 16);             // eth.src = port MAC
-                    nw[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
-                    nw[3] = z[3];
-                    nw[4] = z[4];
-                    nw[5] = 0x0200u | (a.port_mac_lo << 16);                  // op = REPLY, sha
-                    nw[6] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
-                    nw[7] = bswap32(a.port_ip4);                              // spa = port IPv4
-                    nw[8] = at2(z[6], z[5]);                                  // tha = old sha
-                    nw[9] = (z[6] >> 16) | (z[7] << 16);                      // tpa = old spa
-                    nw[10] = (z[7] >> 16) | (z[10] & 0xFFFF0000u);
-                    nw[11] = z[11];
-                    // bytes at or past len keep the buffer's own (never transmitted) bytes
-#pragma unroll
-                    for (int j = 0; j < 12; ++j) {
-                        const uint32_t m = len_mask(len, j);
-                        w[j] = (nw[j] & m) | (w[j] & ~m);
-                    }
-                    if (!(kAblate & 8)) {
-                        uint4* q = reinterpret_cast<uint4*>(p);
-                        q[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                        q[1] = make_uint4(w[4], w[5], w[6], w[7]);
-                        q[2] = make_uint4(w[8], w[9], w[10], w[11]);
-                    }
-                    flags |= UPE_VF_ARP_REPLY;
-                }
-            }
+        // ---- fast path: option-less IPv4 / IPv6 ----
+        const uint32_t e12 = w[3] & 0xFFFFu;          // bytes 12,13 (ethertype, byte-swapped)
+        const bool fast4 = live && len >= 34u && e12 == 0x0008u && byte_of(w[3], 2) == 0x45u;
+        const bool fast6 = live && len >= 54u && e12 == 0xDD86u;
+        Parsed r;
+        r.ok = false; r.consumed = false; r.v6 = fast6; r.flags = 0;
+        r.proto = fast6 ? byte_of(w[5], 0) : byte_of(w[5], 3);              // byte 20 / 23
+        // addresses: v4 host order in word 0 (src/parser.c:40-41); v6 wire bytes
+        r.s[0] = fast6 ? at2(w[6], w[5]) : bswap32(at2(w[7], w[6]));
+        r.d[0] = fast6 ? at2(w[10], w[9]) : bswap32(at2(w[8], w[7]));
+        r.s[1] = at2(w[7], w[6]);  r.s[2] = at2(w[8], w[7]);  r.s[3] = at2(w[9], w[8]);
+        r.d[1] = at2(w[11], w[10]); r.d[2] = at2(w[12], w[11]); r.d[3] = at2(w[13], w[12]);
+        {
+            // L4 at byte 34 (v4) or 54 (v6), both 2 mod 4
+            const uint32_t l4a = fast6 ? at2(w[14], w[13]) : at2(w[9], w[8]);     // L4 0..3
+            const uint32_t l4b = fast6 ? at2(w[15], w[14]) : at2(w[10], w[9]);    // L4 4..7
+            const uint32_t l4c = fast6 ? at2(w[17], w[16]) : at2(w[12], w[11]);   // L4 12..15
+            const uint32_t l4len = len - (fast6 ? 54u : 34u);
+            const uint32_t thl = (byte_of(l4c, 0) >> 4) * 4;
+            const bool udp = r.proto == 17u, tcp = r.proto == 6u, icmp = r.proto == 1u;
+            r.ok = (fast4 || fast6) &&
+                   ((udp || icmp) ? l4len >= 8u
+                                  : tcp && l4len >= 20u && thl >= 20u && l4len >= thl);
+            r.sport = icmp ? be16_lo(l4b) : be16_lo(l4a);                  // icmp: id
+            r.dport = icmp ? be16_lo(l4a) : be16_lo(l4a >> 16);            // type << 8 | code
+            // NDP NS / NA, consumed by handle_control_packet (src/worker.c:57-100)
+            r.consumed = fast6 && len >= 78u && r.proto == 58u &&
+                         ((l4a & 0xFFu) == 135u || (l4a & 0xFFu) == 136u);
         }
-        if (live && is_v6 && len >= 78u && byte_of(w[5], 0) == 58u) {   // src/worker.c:58-100
-            const uint32_t type = byte_of(w[13], 2);                     // byte 54
-            if (type == 135u || type == 136u) consumed = true;
-        }
-        const bool ctrl = live && (consumed || (flags & UPE_VF_ARP_LEARN));
-
-        // ---- parse_flow_key, reference src/parser.c:6-111 ----
-        bool ok = false;
-        uint32_t proto = 0, sport = 0, dport = 0;
-        uint32_t s[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
-        if (live && !consumed && len >= 14u) {
-            if (is_v4) {
-                const uint32_t ver = byte_of(w[3], 2) >> 4;
-                const uint32_t hl = ihl * 4;
-                if (len - 14 >= 20u && ver == 4 && hl >= 20 && len - 14 >= hl) {
-                    proto = byte_of(w[5], 3);                                // byte 23
-                    s[0] = bswap32(at2(w[7], w[6]));                         // bytes 26..29
-                    d[0] = bswap32(at2(w[8], w[7]));                         // bytes 30..33
-                    const uint32_t l4len = len - 14 - hl;
-                    uint32_t l4w0, l4w1, l4w3;
-                    if (ihl == 5) {
-                        l4w0 = at2(w[9], w[8]);    // L4 bytes 0..3  (byte 34)
-                        l4w1 = at2(w[10], w[9]);   // L4 bytes 4..7
-                        l4w3 = at2(w[12], w[11]);  // L4 bytes 12..15
-                    } else {
-                        l4w0 = l4w1 = l4w3 = 0;
-#pragma unroll
-                        for (int h = 6; h <= 15; ++h) {
-                            if ((int)ihl == h) {
-                                l4w0 = at2(w[h + 4], w[h + 3]);
-                                l4w1 = at2(w[h + 5], w[h + 4]);
-                                l4w3 = at2(w[h + 7], w[h + 6]);
-                            }
-                        }
-                    }
-                    if (proto == 17u) {
-                        ok = l4len >= 8u;
-                        sport = be16_lo(l4w0);
-                        dport = be16_lo(l4w0 >> 16);
-                    } else if (proto == 6u) {
-                        const uint32_t thl = (byte_of(l4w3, 0) >> 4) * 4;
-                        ok = l4len >= 20u && thl >= 20u && l4len >= thl;
-                        sport = be16_lo(l4w0);
-                        dport = be16_lo(l4w0 >> 16);
-                    } else if (proto == 1u) {
-                        ok = l4len >= 8u;
-                        sport = be16_lo(l4w1);                               // icmp id
-                        dport = (byte_of(l4w0, 0) << 8) | byte_of(l4w0, 1);  // type << 8 | code
-                    }
-                }
-            } else if (is_v6) {
-                if (len - 14 >= 40u) {
-                    proto = byte_of(w[5], 0);                                // byte 20
-                    s[0] = at2(w[6], w[5]);  s[1] = at2(w[7], w[6]);
-                    s[2] = at2(w[8], w[7]);  s[3] = at2(w[9], w[8]);
-                    d[0] = at2(w[10], w[9]); d[1] = at2(w[11], w[10]);
-                    d[2] = at2(w[12], w[11]); d[3] = at2(w[13], w[12]);
-                    const uint32_t l4len = len - 54;
-                    const uint32_t l4w0 = at2(w[14], w[13]);                 // byte 54
-                    const uint32_t l4w1 = at2(w[15], w[14]);
-                    const uint32_t l4w3 = at2(w[17], w[16]);                 // byte 66
-                    if (proto == 17u) {
-                        ok = l4len >= 8u;
-                        sport = be16_lo(l4w0);
-                        dport = be16_lo(l4w0 >> 16);
-                    } else if (proto == 6u) {
-                        const uint32_t thl = (byte_of(l4w3, 0) >> 4) * 4;
-                        ok = l4len >= 20u && thl >= 20u && l4len >= thl;
-                        sport = be16_lo(l4w0);
-                        dport = be16_lo(l4w0 >> 16);
-                    } else if (proto == 1u) {
-                        ok = l4len >= 8u;
-                        sport = be16_lo(l4w1);
-                        dport = (byte_of(l4w0, 0) << 8) | byte_of(l4w0, 1);
-                    }
-                }
-            }
+        // forward rewrite of bytes 20..27: v4 ttl-- and checksum over the 20-byte header
+        // (src/worker.c:174-176, src/parser.c:137-169, stored LE), v6 hop-- (src/worker.c:213)
+        r.ttl = fast6 ? byte_of(w[5], 1) : byte_of(w[5], 2);               // byte 21 / 22
+        if (fast6) {
+            r.c1w1 = (w[5] & 0xFFFF00FFu) | (((r.ttl - 1) & 0xFFu) << 8);
+            r.c1w2 = w[6];
+        } else {
+            const uint32_t w5n = (w[5] & 0xFF00FFFFu) | (((r.ttl - 1) & 0xFFu) << 16);
+            const uint32_t w6z = w[6] & 0xFFFF0000u;
+            const unsigned long long sum = (unsigned long long)(w[3] >> 16) + w[4] + w5n + w6z +
+                                           w[7] + (w[8] & 0xFFFFu);
+            r.c1w1 = w5n;
+            r.c1w2 = w6z | csum_fold(sum);
         }
 
-        // ---- the forward rewrite of bytes 16..31, computed now so that the header dwords are
-        // dead before the rule scan: IPv4 ttl-- and checksum over IHL*4 bytes
-        // (src/worker.c:174-176, src/parser.c:137-169, stored LE), IPv6 hop-- (src/worker.c:213)
-        const uint32_t ttl = is_v6 ? byte_of(w[5], 1) : byte_of(w[5], 2);   // byte 21 / 22
-        uint32_t c1w1 = w[5], c1w2 = w[6];
-        if (ok && !is_v6 && ttl > 1u) {
-            const uint32_t hw2 = (ttl - 1) | (byte_of(w[5], 3) << 8);       // bytes 22..25
-            unsigned long long sum = 0;
-#pragma unroll
-            for (int j = 0; j < 15; ++j) {
-                const uint32_t dw = j == 2 ? hw2 : at2(w[4 + j], w[3 + j]);
-                if ((uint32_t)j < ihl) sum += dw;
-            }
-            uint32_t f = (uint32_t)(sum & 0xFFFFFFFFull) + (uint32_t)(sum >> 32);
-            f += (uint32_t)(sum & 0xFFFFFFFFull) > f ? 1u : 0u;            // end-around carry
-            f = (f & 0xFFFFu) + (f >> 16);
-            f = (f & 0xFFFFu) + (f >> 16);
-            f = (f & 0xFFFFu) + (f >> 16);
-            const uint32_t cs = (~f) & 0xFFFFu;
-            // bytes 22..25 live in w[5] bytes 2,3 and w[6] bytes 0,1
-            c1w1 = (w[5] & 0x0000FFFFu) | ((ttl - 1) << 16) | (byte_of(w[5], 3) << 24);
-            c1w2 = (w[6] & 0xFFFF0000u) | cs;
-        } else if (ok && is_v6 && ttl > 1u) {
-            c1w1 = (w[5] & 0xFFFF00FFu) | ((ttl - 1) << 8);
+        // ---- general path, for the waves that hold anything else ----
+        const bool slow = live && !fast4 && !fast6;
+        if (__any(slow) && slow) {
+            Parsed g;
+            general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
+            r = g;
         }
+
+        const bool ctrl = live && (r.consumed || (r.flags & UPE_VF_ARP_LEARN));
+        const bool ok = live && r.ok && !r.consumed;
 
         // ---- rule_table_match ----
-        const uint32_t ver = is_v6 ? 6u : 4u;
-        const uint32_t k0 = ver | (proto << 8) | (sport << 16);
-        const uint32_t k1 = dport;
-        const bool need_v6 = __any(ok && is_v6);
+        const uint32_t k0 = (r.v6 ? 6u : 4u) | (r.proto << 8) | (r.sport << 16);
+        const uint32_t k1 = r.dport;
+        const bool need_v6 = __any(ok && r.v6);
         const uint32_t ri = (kAblate & 1) ? (ok ? 0u : kNone)
-                            : need_v6 ? scan_rules<true>(a, !ok, is_v6, k0, k1, s, d)
-                                      : scan_rules<false>(a, !ok, is_v6, k0, k1, s, d);
+                            : need_v6 ? scan_rules<true>(a, !ok, r.v6, k0, k1, r.s, r.d)
+                                      : scan_rules<false>(a, !ok, r.v6, k0, k1, r.s, r.d);
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
-        uint32_t code = 0;
-        uint32_t rbits = 0;
-        if (!live) {
-            code = 0;
-        } else if (consumed) {
+        uint32_t code = 0, rbits = 0;
+        if (r.consumed) {
             code = UPE_V_CONSUMED;
         } else if (!ok) {
             code = UPE_V_DROP_PARSE;
@@ -538,16 +740,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else {
             const int2 info = a.rinfo[ri];
             rbits = (ri + 1) << 8;
-            // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: aggregated per wave below
-            // for LDS-resident tables, direct device atomics for very large ones
+            // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: LDS histogram below for
+            // LDS-resident tables, direct device atomics for very large ones
             if (!(kAblate & 4) && !lds_stats) {
-                atomicAdd(&a.stats[2 * (uint32_t)info.y], 1ull);
-                atomicAdd(&a.stats[2 * (uint32_t)info.y + 1], (unsigned long long)len);
+                atomicAdd(&a.st->stats[2 * (uint32_t)info.y], 1ull);
+                atomicAdd(&a.st->stats[2 * (uint32_t)info.y + 1], (unsigned long long)len);
             }
             code = info.x == UPE_ACT_DROP ? UPE_V_DROP_RULE
                  : info.x == UPE_ACT_FWD  ? UPE_V_FWD
                                           : UPE_V_DROP_ACTION;
         }
+        uint32_t flags = r.flags;
 
         // ---- L3 forward (src/worker.c:155-244) ----
         bool fp4 = false, fp6 = false;       // this packet misses the start entry, hits table
@@ -555,69 +758,60 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         bool hit = false;      // the packet gets a MAC: the table's (or the starting entry's)
         bool cand = false;     // destination == starting L1 entry (ARP: and != 0)
         uint32_t mlo = 0, mhi = 0;
+        bool wrote1 = false;
         if (code == UPE_V_FWD) {
-            if (ttl <= 1u) {                           // src/worker.c:165-172, 204-211
+            if (r.ttl <= 1u) {                         // src/worker.c:165-172, 204-211
                 code = UPE_V_DROP_TTL;
-            } else if (!is_v6) {
-                w[5] = c1w1;
-                w[6] = c1w2;
+            } else if (!r.v6) {
                 wrote1 = true;
-                hit = !(kAblate & 2) && arp_lookup(a.arp, d[0], mlo, mhi);
-                cand = l1_arp_ip != 0 && d[0] == l1_arp_ip;
+                hit = !(kAblate & 2) && arp_lookup(a.arp, r.d[0], mlo, mhi);
+                cand = s_l1[0] != 0 && r.d[0] == s_l1[0];
                 fp4 = !cand && hit;
                 thit4 = hit;
             } else {
-                w[5] = c1w1;
                 wrote1 = true;
-                hit = !(kAblate & 2) && ndp_lookup(a.ndp, d, mlo, mhi);
-                cand = d[0] == l1_ndp[0] && d[1] == l1_ndp[1] && d[2] == l1_ndp[2] &&
-                       d[3] == l1_ndp[3];
+                hit = !(kAblate & 2) && ndp_lookup(a.ndp, r.d, mlo, mhi);
+                cand = r.d[0] == s_l1[1] && r.d[1] == s_l1[2] && r.d[2] == s_l1[3] &&
+                       r.d[3] == s_l1[4];
                 fp6 = !cand && hit;
                 thit6 = hit;
             }
             if (cand) flags |= UPE_VF_L1_INIT;
         }
-
-
-        if (hit) {
-            w[0] = mlo;
-            w[1] = mhi | (a.port_mac_lo << 16);
-            w[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
-            wrote0 = true;
-            flags |= UPE_VF_NEIGH_HIT;
-        }
+        if (hit) flags |= UPE_VF_NEIGH_HIT;
 
         // ---- write back ----
-        if (live) {
-            uint4* q = reinterpret_cast<uint4*>(p);
-            if (kAblate & 8) wrote0 = wrote1 = false;
-            if (wrote0) q[0] = make_uint4(w[0], w[1], w[2], w[3]);
-            if (wrote1) q[1] = make_uint4(w[4], w[5], w[6], w[7]);
-            a.verdict[i] = code | flags | rbits;
+        if (live && !(kAblate & 8)) {
+            uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
+            if (hit)
+                store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
+                                          (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
+            if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
+        if (live) a.verdict[i] = code | flags | rbits;
 
         // ---- rule_stats: LDS histogram (same-address lanes serialise in the LDS atomic unit,
         // cheaper than a cross-lane reduction per distinct rule) ----
-        if (lds_stats && !(kAblate & 4) && live && !consumed && ok && ri != kNone) {
+        if (lds_stats && !(kAblate & 4) && ok && ri != kNone) {
             atomicAdd(&lds_hist[2 * ri], 1u);
             atomicAdd(&lds_hist[2 * ri + 1], len);
         }
 
         // ---- per-wave totals and L1 bookkeeping ----
         const uint32_t wc[C_N] = {
-            (uint32_t)__popcll(__ballot(live && !consumed && ok)),
-            (uint32_t)__popcll(__ballot(live && !consumed && ok && ri != kNone)),
+            (uint32_t)__popcll(__ballot(ok)),
+            (uint32_t)__popcll(__ballot(ok && ri != kNone)),
             (uint32_t)__popcll(__ballot(live && code == UPE_V_FWD)),
             (uint32_t)__popcll(__ballot(live && code != UPE_V_FWD && code != UPE_V_CONSUMED)),
-            (uint32_t)__popcll(__ballot(live && consumed)),
-            (uint32_t)__popcll(__ballot(live && !consumed && (flags & UPE_VF_ARP_LEARN))),
-            (uint32_t)__popcll(__ballot(live && !consumed && (flags & UPE_VF_ARP_REPLY))),
+            (uint32_t)__popcll(__ballot(live && r.consumed)),
+            (uint32_t)__popcll(__ballot(live && !r.consumed && (r.flags & UPE_VF_ARP_LEARN))),
+            (uint32_t)__popcll(__ballot(live && !r.consumed && (r.flags & UPE_VF_ARP_REPLY))),
             (uint32_t)__popcll(__ballot(ctrl)), 0u};
 #pragma unroll
         for (int c = 0; c < C_N; ++c)
             if (lane == 0 && wc[c]) atomicAdd(&s_cnt[c], wc[c]);
         // lane order is packet order, so first / last qualifying packets are ballot bit scans
-        const uint32_t i0 = i - (uint32_t)lane;
+        const uint32_t i0 = tile * kTile + (uint32_t)wave * 64u;
         const unsigned long long bf4 = __ballot(fp4), bf6 = __ballot(fp6), bfc = __ballot(ctrl);
         const unsigned long long bm4 = __ballot(thit4), bm6 = __ballot(thit6);
         const uint32_t f4 = bf4 ? i0 + (uint32_t)__ffsll((long long)bf4) - 1 : kNone;
@@ -626,202 +820,112 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint32_t m4 = bm4 ? i0 + 64u - (uint32_t)__clzll((long long)bm4) : 0u;   // index + 1
         const uint32_t m6 = bm6 ? i0 + 64u - (uint32_t)__clzll((long long)bm6) : 0u;
         // packets the starting entry answers if nothing before them missed it and hit the table
-        const uint32_t cbits = (__ballot(cand && !is_v6 && look4) ? 1u : 0u) |
-                               (__ballot(cand && is_v6 && look6) ? 2u : 0u);
+        const uint32_t cbits = (__ballot(cand && !r.v6 && look4) ? 1u : 0u) |
+                               (__ballot(cand && r.v6 && look6) ? 2u : 0u);
+        // later tiles hold later packets: a hit here supersedes the wave's earlier payload
         if (m4 && i + 1 == m4) {
-            ChunkPay* P = &a.pay[i / 64];
-            P->m4_dst = d[0]; P->m4_mac_lo = mlo; P->m4_mac_hi = mhi;
+            s_pay[wave][0] = r.d[0]; s_pay[wave][1] = mlo; s_pay[wave][2] = mhi;
         }
         if (m6 && i + 1 == m6) {
-            ChunkPay* P = &a.pay[i / 64];
-            P->m6_dst[0] = d[0]; P->m6_dst[1] = d[1]; P->m6_dst[2] = d[2]; P->m6_dst[3] = d[3];
-            P->m6_mac_lo = mlo; P->m6_mac_hi = mhi;
+            s_pay[wave][3] = r.d[0]; s_pay[wave][4] = r.d[1]; s_pay[wave][5] = r.d[2];
+            s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
         }
-        if (lane == 0) {
-            s_red[wave][0] = f4; s_red[wave][1] = f6; s_red[wave][2] = m4;
-            s_red[wave][3] = m6; s_red[wave][4] = fc; s_red[wave][5] = cbits;
+        // wave-uniform: keep the running values in SGPRs
+        wf4 = __builtin_amdgcn_readfirstlane(min(wf4, f4));
+        wf6 = __builtin_amdgcn_readfirstlane(min(wf6, f6));
+        wfc = __builtin_amdgcn_readfirstlane(min(wfc, fc));
+        wm4 = __builtin_amdgcn_readfirstlane(max(wm4, m4));
+        wm6 = __builtin_amdgcn_readfirstlane(max(wm6, m6));
+        if (cbits) {
+            // packets the last workgroup may rewrite: flag the tile, and drain this wave's
+            // stores so the release below covers them
+            if (lane == 0) atomicOr(&a.st->cand_tile[tile], cbits);
+            wcb = __builtin_amdgcn_readfirstlane(wcb | cbits);
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
         }
+    }
+    if (lane == 0) {
+        s_red[wave][0] = wf4; s_red[wave][1] = wf6; s_red[wave][2] = wm4;
+        s_red[wave][3] = wm6; s_red[wave][4] = wfc; s_red[wave][5] = wcb;
     }
     __syncthreads();
 
-    // ---- workgroup flush into the replicated accumulators ----
+    // ---- rule_stats of mid-size tables: straight into the worker totals (the host reads them
+    // after the batch; nothing in this launch does) ----
+    if (lds_stats && !small_stats && !(kAblate & 4)) {
+        for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) {
+            const uint32_t v = lds_hist[k];
+            if (v)
+                atomicAdd(&a.st->stats[2 * (uint32_t)a.rinfo[k >> 1].y + (k & 1)],
+                          (unsigned long long)v);
+        }
+    }
+    if (wave != 0) return;
+
+    // ---- wave 0: flush the workgroup into the replicated accumulators ----
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
     // so every accumulator kind goes out as ONE instruction, lane k carrying field k.
-    if (wave == 0 && !(kAblate & 4)) {
-        uint32_t cb = 0;
+    DevState* S = a.st;
+    const uint32_t rep = blockIdx.x % kReps;
+    uint32_t cb = 0, x4 = 0, x6 = 0;
+    int w4 = 0, w6 = 0;
 #pragma unroll
-        for (int v = 0; v < kWaves; ++v) cb |= s_red[v][5];
-        const bool flag = (look4 || look6) && cb;
+    for (int v = 0; v < kWaves; ++v) {
+        cb |= s_red[v][5];
+        if (s_red[v][2] > x4) { x4 = s_red[v][2]; w4 = v; }
+        if (s_red[v][3] > x6) { x6 = s_red[v][3]; w6 = v; }
+    }
+    const bool flag = (look4 || look6) && cb;
+    if (!(kAblate & 4)) {
         if (lane < C_N) {
             const uint32_t cv = lane == C_CAND ? (flag ? 1u : 0u) : s_cnt[lane];
-            if (cv) atomicAdd(&A->cnt[rep][lane], cv);
+            if (cv) atomicAdd(&S->acc.cnt[rep][lane], cv);
         }
         if (lane < M_N) {
             const int src = lane == M_F4 ? 0 : lane == M_F6 ? 1 : 4;
             uint32_t mv = kNone;
 #pragma unroll
             for (int v = 0; v < kWaves; ++v) mv = min(mv, s_red[v][src]);
-            if (mv != kNone) atomicMin(&A->mins[rep][lane], mv);
+            if (mv != kNone) atomicMin(&S->acc.mins[rep][lane], mv);
         }
         if (lane < X_N) {
-            const int src = lane == X_M4 ? 2 : 3;
-            uint32_t xv = 0;
-#pragma unroll
-            for (int v = 0; v < kWaves; ++v) xv = max(xv, s_red[v][src]);
-            if (xv) atomicMax(&A->maxs[rep][lane], xv);
+            const uint32_t xv = lane == X_M4 ? x4 : x6;
+            if (xv) atomicMax(&S->acc.maxs[rep][lane], xv);
         }
-        if (lane == 0 && (look4 || look6)) a.cand_tile[tile] = cb;
-    }
-    if (lds_stats && !(kAblate & 4)) {
-        if (small_stats) {
-            unsigned long long* out =
-                a.acc_stats + ((size_t)a.parity * kReps + rep) * 2 * a.nrules_pad;
-            for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) {
-                const uint32_t v = lds_hist[r];
-                if (v) atomicAdd(&out[r], (unsigned long long)v);
-            }
-        } else {
-            for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) {
-                const uint32_t v = lds_hist[r];
-                if (v)
-                    atomicAdd(&a.stats[2 * (uint32_t)a.rinfo[r >> 1].y + (r & 1)],
-                              (unsigned long long)v);
+        if (lds_stats && small_stats) {
+            for (uint32_t k = lane; k < 2 * a.nrules_pad; k += 64) {
+                const uint32_t v = lds_hist[k];
+                if (v) atomicAdd(&S->acc_stats[rep][k], (unsigned long long)v);
             }
         }
     }
+    // the workgroup's last table hit per family (only the one holding the batch maximum is read)
+    if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(&S->pay[blockIdx.x]) + lane,
+                           s_pay[lane < 3 ? w4 : w6][lane], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (flag) {
+        // packets here may take the starting entry's answer: publish their verdicts and frames
+        // to the last workgroup (release: write back this XCD's L2)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    // every atomic and payload store of this workgroup is performed before the arrival ticket
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    uint32_t last = 0;
+    if (lane == 0) {
+        const uint32_t nb = gridDim.x;
+        const uint32_t sh = blockIdx.x % kShards;
+        const uint32_t nsh = nb < (uint32_t)kShards ? nb : (uint32_t)kShards;
+        const uint32_t per = nb / kShards + (sh < nb % kShards ? 1u : 0u);
+        if (__hip_atomic_fetch_add(&S->tickets.shard[sh][0], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == per - 1)
+            last = __hip_atomic_fetch_add(&S->tickets.top[0], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+    }
+    if (!__shfl((int)last, 0, 64)) return;
+    batch_tail(a, lane, look4, look6);
 }
 
-// ------------------------------------------------------------------------------------------
-// finalize: fold the batch's accumulators (workgroup 0) and give the starting L1 entry's answer
-// to the packets it answered in the reference (every workgroup, over flagged tiles).
-// ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) upe_finalize(Args a) {
-    if (kAblate & 16) return;
-    // Every global load below is issued in one round before anything waits on it; the running
-    // totals are no-return atomics, so the only dependent round is the L1 payload (and the rare
-    // candidate repair).
-    const int tid = threadIdx.x;
-    const BatchAcc* A = &a.acc[a.parity];
-    const bool blk0 = blockIdx.x == 0;
-    const bool small = blk0 && a.nrules_pad <= (uint32_t)kSmallRules;
-    const uint32_t E = 2 * a.nrules_pad;
-    __shared__ uint32_t s_min[M_N], s_max[X_N];
-    __shared__ unsigned long long s_cnt[C_N];
-    __shared__ unsigned long long s_st[2 * kSmallRules];
-
-    uint32_t mn[M_N], mx[X_N], c[C_N];
-    if (tid < kReps) {
-#pragma unroll
-        for (int j = 0; j < M_N; ++j) mn[j] = A->mins[tid][j];
-#pragma unroll
-        for (int j = 0; j < X_N; ++j) mx[j] = A->maxs[tid][j];
-#pragma unroll
-        for (int j = 0; j < C_N; ++j) c[j] = A->cnt[tid][j];
-    }
-    // small tables: replica r of entry e at acc_stats[parity][r][e]; thread t owns entries
-    // (t + k * kBlock) of the flattened [kReps][E] array
-    constexpr int kStatLoads = kReps * 2 * kSmallRules / kBlock;
-    unsigned long long sv[kStatLoads];
-    const unsigned long long* src = a.acc_stats + (size_t)a.parity * kReps * E;
-#pragma unroll
-    for (int k = 0; k < kStatLoads; ++k) {
-        const uint32_t f = (uint32_t)tid + (uint32_t)k * kBlock;
-        sv[k] = small && f < E * kReps ? src[f] : 0ull;
-    }
-    const uint32_t look = (A->look4 ? 1u : 0u) | (A->look6 ? 2u : 0u);
-
-    if (tid < M_N) s_min[tid] = kNone;
-    if (tid < X_N) s_max[tid] = 0;
-    if (tid < C_N) s_cnt[tid] = 0;
-    if ((uint32_t)tid < 2 * kSmallRules) s_st[tid] = 0;
-    __syncthreads();
-    if (tid < kReps) {
-#pragma unroll
-        for (int j = 0; j < M_N; ++j) atomicMin(&s_min[j], mn[j]);
-#pragma unroll
-        for (int j = 0; j < X_N; ++j) atomicMax(&s_max[j], mx[j]);
-#pragma unroll
-        for (int j = 0; j < C_N; ++j)
-            if (c[j]) atomicAdd(&s_cnt[j], (unsigned long long)c[j]);
-    }
-#pragma unroll
-    for (int k = 0; k < kStatLoads; ++k)
-        if (sv[k]) atomicAdd(&s_st[((uint32_t)tid + (uint32_t)k * kBlock) % E], sv[k]);
-    __syncthreads();
-
-    // Packets whose destination is the starting entry, before the first miss-then-hit packet of
-    // their family, took the entry's MAC (found) in the reference: src/worker.c:186-188, 218-220.
-    if (look && s_cnt[C_CAND] != 0) {
-        const uint32_t f[2] = {s_min[M_F4], s_min[M_F6]};
-        const uint32_t lo[2] = {A->start_arp_lo, A->start_ndp_lo};
-        const uint32_t hi[2] = {A->start_arp_hi, A->start_ndp_hi};
-        __shared__ uint32_t s_list[kBlock];
-        __shared__ uint32_t s_nl;
-        for (uint32_t base = blockIdx.x * kBlock; base < a.ntiles; base += gridDim.x * kBlock) {
-            if (tid == 0) s_nl = 0;
-            __syncthreads();
-            const uint32_t t = base + (uint32_t)tid;
-            const uint32_t cb = t < a.ntiles ? a.cand_tile[t] : 0u;   // flags read in parallel
-            if (cb) s_list[atomicAdd(&s_nl, 1u)] = t;
-            __syncthreads();
-            for (uint32_t k = 0; k < s_nl; ++k) {
-                const uint32_t tt = s_list[k];
-                const uint32_t i = tt * kTile + (uint32_t)tid;
-                if (i >= a.n) continue;
-                const uint32_t v = a.verdict[i];
-                if ((v & 0xFu) != UPE_V_FWD || !(v & UPE_VF_L1_INIT)) continue;
-                uint8_t* p = a.frames + (a.desc[i] >> 16);
-                const int fam = (p[12] == 0x86 && p[13] == 0xDD) ? 1 : 0;
-                if (!((a.cand_tile[tt] >> fam) & 1u) || i >= f[fam]) continue;
-                uint32_t* q = reinterpret_cast<uint32_t*>(p);
-                q[0] = lo[fam];
-                q[1] = hi[fam] | (a.port_mac_lo << 16);
-                q[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
-                a.verdict[i] = v | UPE_VF_NEIGH_HIT;
-            }
-            __syncthreads();
-        }
-    }
-    if (!blk0) return;
-
-    // rule_stats of small tables, in sorted-index space (the host maps index -> rule_id)
-    if (small && (uint32_t)tid < E && s_st[tid]) atomicAdd(&a.stats_idx[tid], s_st[tid]);
-    DevTotals* T = a.totals;
-    if (tid < 8) {
-        const unsigned long long b =
-            tid == 0 ? (unsigned long long)a.n : s_cnt[tid == 1 ? C_PARSED : tid == 2 ? C_MATCHED
-                                                     : tid == 3 ? C_FWD : tid == 4 ? C_DROPPED
-                                                     : tid == 5 ? C_CONSUMED : tid == 6 ? C_ARP_LEARN
-                                                                                : C_ARP_REPLY];
-        if (b) atomicAdd(&T->cnt[tid], b);
-        T->batch[tid] = b;
-    }
-    if (tid == 8) T->n_ctrl = s_cnt[C_CTRL];
-    if (tid == 9)
-        T->first_ctrl = s_min[M_CTRL] == kNone ? ~0ull : (unsigned long long)s_min[M_CTRL];
-    // New L1 state: the last table hit, if some packet missed the starting entry and hit the
-    // table (from then on the cache only ever holds table answers, so it agrees with the
-    // table); otherwise unchanged.
-    DevL1* L = a.l1;
-    if (tid == 16 && s_min[M_F4] != kNone && s_max[X_M4] != 0) {
-        const ChunkPay* P = &a.pay[(s_max[X_M4] - 1) / 64];
-        const uint32_t ip = P->m4_dst, lo = P->m4_mac_lo, hi = P->m4_mac_hi;
-        L->arp_ip = ip;
-        L->arp_mac_lo = lo;
-        L->arp_mac_hi = hi;
-        L->arp_ok = 1;
-    }
-    if (tid == 17 && s_min[M_F6] != kNone && s_max[X_M6] != 0) {
-        const ChunkPay* P = &a.pay[(s_max[X_M6] - 1) / 64];
-        uint32_t ip[4];
-        for (int j = 0; j < 4; ++j) ip[j] = P->m6_dst[j];
-        const uint32_t lo = P->m6_mac_lo, hi = P->m6_mac_hi;
-        for (int j = 0; j < 4; ++j) L->ndp_ip[j] = ip[j];
-        L->ndp_mac_lo = lo;
-        L->ndp_mac_hi = hi;
-        L->ndp_ok = 1;
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // host side
@@ -858,7 +962,6 @@ struct upe_gpu_ctx {
     int2* rinfo = nullptr;
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
-    unsigned long long* acc_stats = nullptr;   // [2][kReps][rules_alloc][2] (small tables)
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
     std::vector<int2> rinfo_host;              // (action, rule_id) per sorted index
     // neighbour tables (reachable-entry indexes)
@@ -866,23 +969,28 @@ struct upe_gpu_ctx {
     uint32_t arp_bits = 0, arp_seed = 0;
     uint4* ndp = nullptr;
     uint32_t ndp_bits = 0, ndp_seed = 0;
-    // state
+    // state: one DevState allocation; the named members are device addresses inside it
+    DevState* st = nullptr;
     DevL1* l1 = nullptr;
     DevTotals* totals = nullptr;
-    unsigned long long* stats = nullptr;   // [cap][2]
     BatchAcc* acc = nullptr;
+    Tickets* tickets = nullptr;
+    unsigned long long* acc_stats = nullptr;   // [kReps][2 * kSmallRules] (small tables)
+    unsigned long long* stats = nullptr;   // [cap][2]
     // per-batch scratch
-    ChunkPay* pay = nullptr;       // [ntiles * kWaves]
-    uint32_t* cand_tile = nullptr; // [ntiles]
+    TilePay* pay = nullptr;        // [ntiles]
+    uint32_t* cand_tile = nullptr; // [ntiles], zero between batches
     size_t tiles_alloc = 0;
-    uint32_t epoch = 0;
     int cus = 256;
+    uint32_t resident = 0;         // persistent grid size for resident_lds bytes of dynamic LDS
+    size_t resident_lds = 0;
+    int blocks_per_cu_override = 0;   // UPE_GPU_BLOCKS_PER_CU (diagnostic)
     uint32_t port_mac_lo = 0, port_mac_hi = 0, port_ip4 = 0;
     bool have_batch = false;
     // kernel timing (upe_gpu_timing_*)
     bool timing = false;
     uint32_t timing_every = 1, timing_calls = 0;   // sample every n-th process() call
-    std::vector<hipEvent_t> ev;   // event pool, 3 per process() call: start, mid, end
+    std::vector<hipEvent_t> ev;   // event pool, 2 per timed process() call
     size_t ev_used = 0;
 };
 
@@ -935,6 +1043,21 @@ int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& see
     return -1;
 }
 
+// Point the DevState at the separately allocated arrays (after any of them is reallocated).
+int publish(upe_gpu_ctx* c) {
+    struct {
+        TilePay* pay;
+        uint32_t* cand_tile;
+        unsigned long long* stats;
+        unsigned long long* stats_idx;
+    } p = {c->pay, c->cand_tile, c->stats, c->stats_idx};
+    static_assert(offsetof(DevState, stats_idx) - offsetof(DevState, pay) == 3 * sizeof(void*),
+                  "DevState pointer block");
+    HIP_TRY(hipMemcpy(reinterpret_cast<char*>(c->st) + offsetof(DevState, pay), &p, sizeof p,
+                      hipMemcpyHostToDevice));
+    return 0;
+}
+
 int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
     if (ntiles > c->tiles_alloc) {
         if (c->pay) (void)hipFree(c->pay);
@@ -943,9 +1066,11 @@ int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
         c->cand_tile = nullptr;
         c->tiles_alloc = 0;
         size_t want = ntiles + ntiles / 4 + 16;
-        HIP_TRY(hipMalloc(&c->pay, want * kWaves * sizeof(ChunkPay)));
+        HIP_TRY(hipMalloc(&c->pay, want * sizeof(TilePay)));
         HIP_TRY(hipMalloc(&c->cand_tile, want * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(c->cand_tile, 0, want * sizeof(uint32_t)));
         c->tiles_alloc = want;
+        if (publish(c) != 0) return -1;
     }
     return 0;
 }
@@ -957,12 +1082,15 @@ int refresh(upe_gpu_ctx* c) {
     return 0;
 }
 
+// Accumulators, small-table stats replicas and arrival tickets in their between-batch state
+// (every batch's last workgroup leaves them so).
 int arm_acc(upe_gpu_ctx* c) {
-    HIP_TRY(hipMemsetAsync(c->acc, 0, 2 * sizeof(BatchAcc), c->stream));
-    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(c->acc + 1) + offsetof(BatchAcc, mins), 0xFF,
-                           sizeof(((BatchAcc*)nullptr)->mins), c->stream));
+    HIP_TRY(hipMemsetAsync(c->acc, 0, sizeof(BatchAcc), c->stream));
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(c->acc) + offsetof(BatchAcc, mins), 0xFF,
                            sizeof(((BatchAcc*)nullptr)->mins), c->stream));
+    HIP_TRY(hipMemsetAsync(c->tickets, 0, sizeof(Tickets), c->stream));
+    HIP_TRY(hipMemsetAsync(c->acc_stats, 0,
+                           (size_t)kReps * kSmallRules * 2 * sizeof(unsigned long long), c->stream));
     return 0;
 }
 
@@ -1002,16 +1130,21 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
     if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return bad(e, "hipStreamCreate");
-    if ((e = hipMalloc(&c->l1, sizeof(DevL1))) != hipSuccess) return bad(e, "hipMalloc l1");
-    if ((e = hipMalloc(&c->totals, sizeof(DevTotals))) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMalloc(&c->st, sizeof(DevState))) != hipSuccess) return bad(e, "hipMalloc state");
+    if ((e = hipMemset(c->st, 0, sizeof(DevState))) != hipSuccess) return bad(e, "hipMemset");
+    c->l1 = &c->st->l1;
+    c->totals = &c->st->totals;
+    c->acc = &c->st->acc;
+    c->tickets = &c->st->tickets;
+    c->acc_stats = &c->st->acc_stats[0][0];
     if ((e = hipMalloc(&c->stats, rule_capacity * 2 * sizeof(unsigned long long))) != hipSuccess)
         return bad(e, "hipMalloc stats");
-    if ((e = hipMalloc(&c->acc, 2 * sizeof(BatchAcc))) != hipSuccess) return bad(e, "hipMalloc acc");
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
                 hipSuccess && cus > 0)
             c->cus = cus;
+        if (const char* v = getenv("UPE_GPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = atoi(v);
     }
     if (arm_acc(c) != 0) {
         std::string m = g_err;
@@ -1045,8 +1178,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->acc_stats, c->stats_idx, c->arp, c->ndp, c->l1,
-                    c->totals, c->stats, c->acc, c->pay, c->cand_tile};
+    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
+                    c->pay, c->cand_tile};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1114,12 +1247,15 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         a.s0 = le32(si) & a.sm0;
         a.dm0 = le32(dm);
         a.d0 = le32(di) & a.dm0;
+        bool v6w = false;
         for (int j = 0; j < 3; ++j) {
             b.sm[j] = le32(sm + 4 * (j + 1));
             b.s[j] = le32(si + 4 * (j + 1)) & b.sm[j];
             b.dm[j] = le32(dm + 4 * (j + 1));
             b.d[j] = le32(di + 4 * (j + 1)) & b.dm[j];
+            v6w |= b.sm[j] != 0 || b.dm[j] != 0;
         }
+        if (v6w) a.m1 |= kRuleV6Words;   // IPv6 keys must test this rule's rv6 words
         info[i] = make_int2(r.action.type, (int)r.rule_id);
     }
     HIP_TRY(hipStreamSynchronize(c->stream));   // previous batches may still read the table
@@ -1128,28 +1264,21 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         if (c->rv4) (void)hipFree(c->rv4);
         if (c->rv6) (void)hipFree(c->rv6);
         if (c->rinfo) (void)hipFree(c->rinfo);
-        if (c->acc_stats) (void)hipFree(c->acc_stats);
-        c->rv4 = nullptr; c->rv6 = nullptr; c->rinfo = nullptr; c->acc_stats = nullptr;
+        c->rv4 = nullptr; c->rv6 = nullptr; c->rinfo = nullptr;
         c->rules_alloc = 0;
         HIP_TRY(hipMalloc(&c->rv4, pad * sizeof(RuleV4)));
         HIP_TRY(hipMalloc(&c->rv6, pad * sizeof(RuleV6)));
         HIP_TRY(hipMalloc(&c->rinfo, pad * sizeof(int2)));
-        const size_t acc_words = pad <= (size_t)kSmallRules ? 2 * (size_t)kReps * pad * 2 : 2;
-        HIP_TRY(hipMalloc(&c->acc_stats, acc_words * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(c->acc_stats, 0, acc_words * sizeof(unsigned long long)));
         if (c->stats_idx) (void)hipFree(c->stats_idx);
         c->stats_idx = nullptr;
         HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * sizeof(unsigned long long)));
         HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * sizeof(unsigned long long)));
         c->rules_alloc = pad;
+        if (publish(c) != 0) return -1;
     }
     HIP_TRY(hipMemcpy(c->rv4, v4.data(), pad * sizeof(RuleV4), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->rv6, v6.data(), pad * sizeof(RuleV6), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->rinfo, info.data(), pad * sizeof(int2), hipMemcpyHostToDevice));
-    if (pad <= (size_t)kSmallRules && c->nrules_pad != (uint32_t)pad) {
-        // accumulator rows are indexed with the padded count: clear them for the new layout
-        HIP_TRY(hipMemset(c->acc_stats, 0, 2 * (size_t)kReps * pad * 2 * sizeof(unsigned long long)));
-    }
     c->nrules = (uint32_t)count;
     c->nrules_pad = (uint32_t)pad;
     c->rinfo_host = info;
@@ -1300,16 +1429,16 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
         HIP_TRY(hipStreamWaitEvent(s, dep, 0));
         HIP_TRY(hipEventDestroy(dep));
     }
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
     const bool timed = c->timing && (c->timing_calls++ % c->timing_every) == 0;
     if (timed) {
-        while (c->ev.size() < c->ev_used + 3) {
+        while (c->ev.size() < c->ev_used + 2) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             c->ev.push_back(e);
         }
-        for (int j = 0; j < 3; ++j) ev[j] = c->ev[c->ev_used + j];
-        c->ev_used += 3;
+        for (int j = 0; j < 2; ++j) ev[j] = c->ev[c->ev_used + j];
+        c->ev_used += 2;
         HIP_TRY(hipEventRecord(ev[0], s));
     }
     Args a;
@@ -1318,36 +1447,31 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     a.verdict = d_verdict;
     a.n = (uint32_t)n;
     a.ntiles = ntiles;
-    a.parity = (++c->epoch) & 1u;
     a.rv4 = c->rv4;
     a.rv6 = c->rv6;
     a.rinfo = c->rinfo;
     a.nrules_pad = c->nrules_pad;
     a.arp = arp_index(c);
     a.ndp = ndp_index(c);
-    a.l1 = c->l1;
-    a.acc = c->acc;
-    a.pay = c->pay;
-    a.cand_tile = c->cand_tile;
-    a.acc_stats = c->acc_stats;
-    a.stats = c->stats;
-    a.stats_idx = c->stats_idx;
-    a.totals = c->totals;
+    a.st = c->st;
     a.port_mac_lo = c->port_mac_lo;
     a.port_mac_hi = c->port_mac_hi;
     a.port_ip4 = c->port_ip4;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     const size_t lds = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
-    const uint32_t grid = ntiles ? ntiles : 1;
+    // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
+    if (c->resident_lds != lds || c->resident == 0) {
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify, kBlock, lds));
+        if (per_cu < 1) per_cu = 1;
+        if (c->blocks_per_cu_override > 0) per_cu = c->blocks_per_cu_override;
+        c->resident = (uint32_t)per_cu * (uint32_t)c->cus;
+        c->resident_lds = lds;
+    }
+    const uint32_t grid = ntiles == 0 ? 1u : ntiles < c->resident ? ntiles : c->resident;
     hipLaunchKernelGGL(upe_classify, dim3(grid), dim3(kBlock), lds, s, a);
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(ev[1], s));
-    const uint32_t fgrid = grid < 256 ? grid : 256;
-    if (!(kAblate & 32)) {
-        hipLaunchKernelGGL(upe_finalize, dim3(fgrid), dim3(kBlock), 0, s, a);
-        HIP_TRY(hipGetLastError());
-    }
-    if (timed) HIP_TRY(hipEventRecord(ev[2], s));
     c->have_batch = true;
     return 0;
 }
@@ -1438,17 +1562,15 @@ int upe_gpu_timing_read(upe_gpu_ctx_t* c, double* classify_ms, double* finalize_
     if (!c) return fail("null context");
     HIP_TRY(hipSetDevice(c->device));
     double a = 0, b = 0;
-    for (size_t j = 0; j + 3 <= c->ev_used; j += 3) {
-        HIP_TRY(hipEventSynchronize(c->ev[j + 2]));
-        float x = 0, y = 0;
+    for (size_t j = 0; j + 2 <= c->ev_used; j += 2) {
+        HIP_TRY(hipEventSynchronize(c->ev[j + 1]));
+        float x = 0;
         HIP_TRY(hipEventElapsedTime(&x, c->ev[j], c->ev[j + 1]));
-        HIP_TRY(hipEventElapsedTime(&y, c->ev[j + 1], c->ev[j + 2]));
         a += x;
-        b += y;
     }
     if (classify_ms) *classify_ms = a;
     if (finalize_ms) *finalize_ms = b;
-    if (launches) *launches = c->ev_used / 3;
+    if (launches) *launches = c->ev_used / 2;
     return 0;
 }
 
