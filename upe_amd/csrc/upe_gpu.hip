@@ -79,6 +79,9 @@ constexpr int kLdsStatsMax = 4096;     // rule_stats histogrammed in LDS up to t
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kShards = 8;             // arrival-ticket shards
+#ifndef UPE_GLDS
+#define UPE_GLDS 0   // header windows by LDS-DMA (0: per-lane 16-byte loads, for A/B timing)
+#endif
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
@@ -471,63 +474,95 @@ __device__ __noinline__ void general_path(Port a, uint8_t* p, uint32_t len, Pars
 }
 
 // ------------------------------------------------------------------------------------------
-// The batch's last workgroup (wave 0, every other workgroup has arrived): fold the accumulators
-// into the worker totals, update the L1 state, give the starting L1 entry's answer to the
-// packets it answered in the reference, and re-arm accumulators and tickets for the next batch.
+// The batch's last workgroup (all its threads, every other workgroup has arrived): fold the
+// accumulators into the worker totals, update the L1 state, give the starting L1 entry's answer
+// to the packets it answered in the reference, and re-arm accumulators and tickets for the next
+// batch.  Every read is issued before any result is used, so the fold costs one memory round
+// trip (plus one per 1024 words of small-table rule_stats), not one per word.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void batch_tail(const Args& a, int lane, bool look4, bool look6) {
+__device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, bool look6) {
     __shared__ unsigned long long t_cnt[C_N];
     __shared__ uint32_t t_min[M_N], t_max[X_N];
     __shared__ unsigned long long t_st[2 * kSmallRules];
+    __shared__ uint32_t t_pay[kPayWords];
     DevState* S = a.st;
+    const int lane = tid & 63;
     const bool small = a.nrules_pad <= (uint32_t)kSmallRules;
     const uint32_t E = 2 * a.nrules_pad;
-    if (lane < C_N) t_cnt[lane] = 0;
-    if (lane < M_N) t_min[lane] = kNone;
-    if (lane < X_N) t_max[lane] = 0;
-    for (uint32_t e = lane; e < 2 * kSmallRules; e += 64) t_st[e] = 0;
-    __builtin_amdgcn_wave_barrier();
+    if (tid < C_N) t_cnt[tid] = 0;
+    if (tid < M_N) t_min[tid] = kNone;
+    if (tid < X_N) t_max[tid] = 0;
+    for (uint32_t e = tid; e < 2 * kSmallRules; e += kBlock) t_st[e] = 0;
+    __syncthreads();
 
     // accumulators: read and re-arm in one atomic exchange per word (reads the value every
     // workgroup's atomics left, whichever XCD they ran on)
     uint32_t* accw = reinterpret_cast<uint32_t*>(&S->acc);
     constexpr uint32_t kCntW = kReps * C_N, kMinW = kReps * M_N, kAccW = kReps * kAccFields;
-    for (uint32_t k = lane; k < kAccW; k += 64) {
+    constexpr int kAccPer = (int)((kAccW + kBlock - 1) / kBlock);
+    uint32_t av[kAccPer];
+#pragma unroll
+    for (int j = 0; j < kAccPer; ++j) {
+        const uint32_t k = (uint32_t)tid + (uint32_t)j * kBlock;
         const bool is_min = k >= kCntW && k < kCntW + kMinW;
-        const uint32_t v = __hip_atomic_exchange(&accw[k], is_min ? kNone : 0u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+        av[j] = k < kAccW ? __hip_atomic_exchange(&accw[k], is_min ? kNone : 0u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                          : 0u;
+    }
+    // The workgroup that took the batch's last tile most likely holds the batch's last table
+    // hits: read its payload now, speculatively (used only if it is the right one).
+    const uint32_t spec = (a.ntiles - 1) % gridDim.x;
+    uint32_t pv = 0;
+    if (tid < kPayWords)
+        pv = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&S->pay[spec]) + tid,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // small-table rule_stats replicas, kStPer words per thread per round
+    constexpr int kStPer = 4;
+    const uint32_t EW = small ? E * kReps : 0u;
+    for (uint32_t base = 0; base < EW; base += kStPer * kBlock) {
+        unsigned long long sv[kStPer];
+#pragma unroll
+        for (int j = 0; j < kStPer; ++j) {
+            const uint32_t k = base + (uint32_t)tid + (uint32_t)j * kBlock;
+            sv[j] = k < EW ? __hip_atomic_exchange(&S->acc_stats[k / E][k % E], 0ull,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < kStPer; ++j) {
+            const uint32_t k = base + (uint32_t)tid + (uint32_t)j * kBlock;
+            if (sv[j]) atomicAdd(&t_st[k % E], sv[j]);
+        }
+    }
+    if (tid < kPayWords) t_pay[tid] = pv;
+#pragma unroll
+    for (int j = 0; j < kAccPer; ++j) {
+        const uint32_t k = (uint32_t)tid + (uint32_t)j * kBlock;
+        const uint32_t v = av[j];
+        if (k >= kAccW) continue;
         if (k < kCntW) {
             if (v) atomicAdd(&t_cnt[k % C_N], (unsigned long long)v);
-        } else if (is_min) {
-            atomicMin(&t_min[(k - kCntW) % M_N], v);
+        } else if (k < kCntW + kMinW) {
+            if (v != kNone) atomicMin(&t_min[(k - kCntW) % M_N], v);
         } else {
-            atomicMax(&t_max[(k - kCntW - kMinW) % X_N], v);
+            if (v) atomicMax(&t_max[(k - kCntW - kMinW) % X_N], v);
         }
     }
-    if (small) {
-        for (uint32_t k = lane; k < E * kReps; k += 64) {
-            const unsigned long long v = __hip_atomic_exchange(
-                &S->acc_stats[k / E][k % E], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v) atomicAdd(&t_st[k % E], v);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // LDS results visible to the wave
+    __syncthreads();
 
     // worker totals and this batch's summary
-    if (small && (uint32_t)lane < E && t_st[lane]) atomicAdd(&S->stats_idx[lane], t_st[lane]);
-    if (small && (uint32_t)lane + 64 < E && t_st[lane + 64])
-        atomicAdd(&S->stats_idx[lane + 64], t_st[lane + 64]);
+    if (small && (uint32_t)tid < E && t_st[tid]) atomicAdd(&S->stats_idx[tid], t_st[tid]);
     DevTotals* T = &S->totals;
-    if (lane < 8) {
+    if (tid < 8) {
         // upe_counters_t order: pkts_in, then C_PARSED .. C_ARP_REPLY
-        const unsigned long long b = lane == 0 ? (unsigned long long)a.n : t_cnt[lane - 1];
-        if (b) atomicAdd(&T->cnt[lane], b);
-        T->batch[lane] = b;
+        const unsigned long long b = tid == 0 ? (unsigned long long)a.n : t_cnt[tid - 1];
+        if (b) atomicAdd(&T->cnt[tid], b);
+        T->batch[tid] = b;
     }
-    if (lane == 8) T->n_ctrl = t_cnt[C_CTRL];
-    if (lane == 9)
+    if (tid == 8) T->n_ctrl = t_cnt[C_CTRL];
+    if (tid == 9)
         T->first_ctrl = t_min[M_CTRL] == kNone ? ~0ull : (unsigned long long)t_min[M_CTRL];
+    if (tid >= 64) return;   // wave 0 does the rest
 
     // Packets whose destination is the starting entry, before the first miss-then-hit packet of
     // their family, took the entry's MAC (found) in the reference: src/worker.c:186-188, 218-220.
@@ -579,22 +614,25 @@ __device__ __forceinline__ void batch_tail(const Args& a, int lane, bool look4, 
     // table (from then on the cache only ever holds table answers, so it agrees with the
     // table); otherwise unchanged.
     if (lane == 0 && t_min[M_F4] != kNone && t_max[X_M4] != 0) {
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(
-            &S->pay[((t_max[X_M4] - 1) / kTile) % gridDim.x]);
+        const uint32_t wg = ((t_max[X_M4] - 1) / kTile) % gridDim.x;
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(&S->pay[wg]);
         uint32_t v[3];
         for (int j = 0; j < 3; ++j)
-            v[j] = __hip_atomic_load(P + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = wg == spec ? t_pay[j]
+                              : __hip_atomic_load(P + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         L->arp_ip = v[0];
         L->arp_mac_lo = v[1];
         L->arp_mac_hi = v[2];
         L->arp_ok = 1;
     }
     if (lane == 1 && t_min[M_F6] != kNone && t_max[X_M6] != 0) {
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(
-            &S->pay[((t_max[X_M6] - 1) / kTile) % gridDim.x]);
+        const uint32_t wg = ((t_max[X_M6] - 1) / kTile) % gridDim.x;
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(&S->pay[wg]);
         uint32_t v[6];
         for (int j = 0; j < 6; ++j)
-            v[j] = __hip_atomic_load(P + 3 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = wg == spec ? t_pay[3 + j]
+                              : __hip_atomic_load(P + 3 + j, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
         for (int j = 0; j < 4; ++j) L->ndp_ip[j] = v[j];
         L->ndp_mac_lo = v[4];
         L->ndp_mac_hi = v[5];
@@ -617,6 +655,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ uint32_t s_red[kWaves][8];
     __shared__ uint32_t s_pay[kWaves][kPayWords];
     __shared__ uint32_t s_l1[8];   // starting L1 entries: arp ip, ndp ip[4], look flags
+    __shared__ uint32_t s_last;    // this workgroup arrived last (set by wave 0)
+#if UPE_GLDS
+    __shared__ uint4 s_win[kWaves][256];   // per wave: 64 frames x bytes 0..63 (LDS-DMA target)
+#endif
 
     if (kAblate & 64) return;
     const int tid = threadIdx.x;
@@ -644,26 +686,73 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
     // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
     // workgroup, at the very end of its life, not once per tile.
+    // descriptors run one tile ahead of the frames they point at
+    uint64_t dsc_next = 0;
+    if (blockIdx.x < a.ntiles && blockIdx.x * kTile + (uint32_t)tid < a.n)
+        dsc_next = a.desc[blockIdx.x * kTile + (uint32_t)tid];
     for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint32_t i = tile * kTile + (uint32_t)tid;
         const bool live = i < a.n;
-        const uint64_t dsc = live ? a.desc[i] : 0;
+        const uint64_t dsc = dsc_next;
         const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
         // frames are 16-byte aligned: the offset in 16-byte units fits one register
         const uint32_t off16 = (uint32_t)(dsc >> 20);
         uint8_t* p = a.frames + ((size_t)off16 << 4);
 
-        // ---- header window: bytes 0..79, five 16-byte loads issued together ----
+        // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past
+        // len are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame
+        // costs four loads, not five.  Frames shorter than 49 bytes never take the fast path.
         uint32_t w[20];
 #pragma unroll
         for (int j = 0; j < 20; ++j) w[j] = 0;
+#if UPE_GLDS
+        {
+            // Bytes 0..63 of the wave's 64 frames arrive by LDS-DMA in four fully coalesced
+            // wave-instructions (16 frames x 64 B each, contiguous for packed frames), not as
+            // 64-byte-strided per-lane loads: each line leaves L2 once.  Slot P of this wave's
+            // window holds chunk (P & 3) ^ ((P >> 4) & 3) of frame P >> 2, so that the per-lane
+            // read-back below is free of LDS bank conflicts.
+            const uint32_t wbase = tile * kTile + (uint32_t)wave * 64u;
+            const uint8_t* fr = a.frames;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int P = 64 * k + lane;
+                const int j = P >> 2;
+                const int c = (P & 3) ^ ((j >> 2) & 3);
+                const uint32_t offj = (uint32_t)__shfl((int)off16, j, 64);
+                if (wbase + (uint32_t)j < a.n)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(fr + ((size_t)offj << 4) +
+                                                                        16 * c),
+                        (__attribute__((address_space(3))) void*)&s_win[wave][64 * k], 16, 0, 0);
+            }
+            uint4 c4 = make_uint4(0, 0, 0, 0);
+            if (live && len > 64u) c4 = reinterpret_cast<const uint4*>(p)[4];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint4 v = s_win[wave][4 * lane + (c ^ ((lane >> 2) & 3))];
+                if (!live || (c == 3 && len <= 48u)) v = make_uint4(0, 0, 0, 0);
+                w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+            }
+            w[16] = c4.x; w[17] = c4.y; w[18] = c4.z; w[19] = c4.w;
+        }
+#else
         if (live) {
             const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
-                const uint4 v = q[c];
-                w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+                if (c < 3 || len > 16u * c) {
+                    const uint4 v = q[c];
+                    w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+                }
             }
+        }
+#endif
+        {
+            const uint32_t nt = tile + gridDim.x;
+            dsc_next = 0;
+            if (nt < a.ntiles && nt * kTile + (uint32_t)tid < a.n) dsc_next = a.desc[nt * kTile + tid];
         }
 
         // ---- fast path: option-less IPv4 / IPv6 ----
@@ -860,8 +949,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                           (unsigned long long)v);
         }
     }
-    if (wave != 0) return;
-
+    if (wave == 0) {
     // ---- wave 0: flush the workgroup into the replicated accumulators ----
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
     // so every accumulator kind goes out as ONE instruction, lane k carrying field k.
@@ -922,8 +1010,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             last = __hip_atomic_fetch_add(&S->tickets.top[0], 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
     }
-    if (!__shfl((int)last, 0, 64)) return;
-    batch_tail(a, lane, look4, look6);
+    if (lane == 0) s_last = last;
+    }   // wave 0
+    // the other waves wait here, so the last workgroup folds the batch with all its threads
+    __syncthreads();
+    if (!s_last) return;
+    batch_tail(a, tid, look4, look6);
 }
 
 
