@@ -93,6 +93,43 @@ def cpu_baseline(wl, threads: int) -> dict:
             "sample": sample}
 
 
+def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
+    """Host-inclusive rate: the batch starts and ends in pinned host memory (libpcap in, AF_PACKET
+    out): upe_gpu_process_host pipelines H2D of frames + descriptors, classify and D2H of verdicts
+    + rewritten header bytes over chunks.  windows: ship 96-byte header windows, not frames."""
+    from upe_amd import gpu, synth
+    from upe_amd.layout import FRAME_TAIL, REWRITE_EXTENT, desc_lens, desc_offsets
+
+    src = synth.header_windows(wl) if windows else wl
+    pf = gpu.PinnedArray(src.frames.shape, np.uint8)
+    pd = gpu.PinnedArray(src.desc.shape, np.uint64)
+    pv = gpu.PinnedArray((wl.n,), np.uint32)
+    pd.array[:] = src.desc
+    times = []
+    for r in range(reps + 2):
+        pf.array[:] = src.frames          # untimed: a fresh batch every pass
+        t0 = time.perf_counter()
+        worker.process_host(pf.array, pd.array, pv.array, chunk)
+        t1 = time.perf_counter()
+        if r >= 2:
+            times.append(t1 - t0)
+    for x in (pf, pd, pv):
+        x.free()
+    t = float(np.median(times))
+    # bytes the copies actually move: per chunk the frame span in, and back the span up to the
+    # last rewritable byte (UPE_REWRITE_EXTENT) plus the verdicts
+    lens = desc_lens(src.desc)
+    offs = desc_offsets(src.desc)
+    ck = chunk or (1 << 18)
+    h2d = d2h = 0
+    for s in range(0, wl.n, ck):
+        o, ln = offs[s:s + ck], lens[s:s + ck]
+        h2d += int(o.max() + FRAME_TAIL - o.min()) + 8 * len(o)
+        d2h += int((o + np.minimum(ln, REWRITE_EXTENT)).max() - o.min()) + 4 * len(o)
+    return {"seconds": t, "packets": wl.n, "h2d_bytes": h2d, "d2h_bytes": d2h,
+            "windows": windows, "chunk": chunk or (1 << 18), "reps": reps}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,6 +140,9 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-copies", type=int, default=1024)
+    ap.add_argument("--host-reps", type=int, default=10,
+                    help="passes of the host round-trip leg (0: skip it)")
+    ap.add_argument("--host-chunk", type=int, default=0)
     args = ap.parse_args()
 
     import torch
@@ -173,6 +213,15 @@ def main() -> None:
     classify_ms, finalize_ms, launches = worker.timing_read()
     worker.timing_enable(False)
 
+    # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
+    worker.reset_stats()
+    hr = None
+    if args.host_reps > 0:
+        if dist:
+            dist.barrier()
+        hr = host_roundtrip(worker, wl, args.host_reps, args.host_chunk,
+                            windows=args.config != "B")
+
     elapsed = t1 - t0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -181,6 +230,10 @@ def main() -> None:
         tot = torch.tensor([n * args.steps], dtype=torch.float64, device=dev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         total_packets = float(tot.item())
+        if hr:
+            ht = torch.tensor([hr["seconds"]], dtype=torch.float64, device=dev)
+            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
+            hr["seconds"] = float(ht.item())
     else:
         total_packets = float(n * args.steps)
 
@@ -222,6 +275,19 @@ def main() -> None:
                 "event_samples": int(launches),
             },
         }
+        if hr:
+            out["host_roundtrip"] = {
+                "value": round(hr["packets"] * world / hr["seconds"] / 1e6, 2), "unit": "Mpps",
+                "ms_per_batch": round(hr["seconds"] * 1e3, 3),
+                "h2d_GBps": round(hr["h2d_bytes"] / hr["seconds"] / 1e9, 2),
+                "d2h_GBps": round(hr["d2h_bytes"] / hr["seconds"] / 1e9, 2),
+                "h2d_bytes_per_packet": round(hr["h2d_bytes"] / hr["packets"], 1),
+                "d2h_bytes_per_packet": round(hr["d2h_bytes"] / hr["packets"], 1),
+                "header_windows": hr["windows"], "chunk": hr["chunk"],
+                "what": "pinned host batch -> H2D -> classify -> D2H of verdicts + rewritten "
+                        "header bytes, 3-slot pipeline (upe_gpu_process_host); median of "
+                        f"{hr['reps']} passes, all ranks at once",
+            }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
         print(json.dumps(out), flush=True)

@@ -212,6 +212,28 @@ int upe_gpu_get_l1(upe_gpu_ctx_t *ctx, upe_l1_state_t *l1);
 int upe_gpu_process(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                     uint32_t *d_verdict, size_t n, void *stream);
 
+/* Host round trip: process n packets that live in HOST memory, the way the path runs between
+ * libpcap (reference src/rx_pcap.c:42-93 fills pktbufs in host memory) and AF_PACKET TX
+ * (src/tx_afpacket.c:78-118 sends from host memory).  The batch is cut into chunks of `chunk`
+ * packets (0 = 256k) pipelined through three device slots: chunk k+1's frames and descriptors go
+ * host->device on a copy stream while chunk k is classified on the context's stream and chunk
+ * k-1's verdicts and rewritten header bytes go device->host on a second copy stream.  Chunks are
+ * classified in order, so counters, rule_stats and the L1 state evolve exactly as for
+ * back-to-back upe_gpu_process() batches of `chunk` packets (upe_gpu_batch_info() describes the
+ * last chunk).  h_frames / h_desc follow the "Batch layout" (offsets relative to h_frames,
+ * frames_bytes covering UPE_FRAME_TAIL bytes past every frame start); a frame may be a header
+ * window (UPE_HDR_WINDOW), which is how a caller avoids shipping payloads.  Only the first
+ * min(len, UPE_REWRITE_EXTENT) bytes of a frame can change; those are copied back in place.
+ * Synchronous.  Buffers from upe_gpu_host_alloc() (pinned) give the full PCIe rate; pageable
+ * buffers work at the staged-copy rate. */
+#define UPE_REWRITE_EXTENT 48
+int upe_gpu_process_host(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_bytes,
+                         const uint64_t *h_desc, uint32_t *h_verdict, size_t n, size_t chunk);
+
+/* Pinned (page-locked) host memory for upe_gpu_process_host() batches. */
+void *upe_gpu_host_alloc(size_t bytes);
+int upe_gpu_host_free(void *ptr);
+
 /* Wait for all work queued on the context's stream (or `stream`). */
 int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
 

@@ -1,0 +1,105 @@
+"""GPU parity of the host round trip (upe_gpu_process_host: host batch -> H2D -> classify ->
+D2H of verdicts and rewritten header bytes, pipelined in chunks), against the reference's golden
+vectors and the oracle.  Chunked processing must equal back-to-back batches, i.e. the reference
+worker's sequential result (only UPE_VF_L1_INIT is relative to each chunk's start)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import golden_io
+import oracle
+from upe_amd import gpu, synth
+from upe_amd.layout import REWRITE_EXTENT, desc_lens, desc_offsets
+
+pytestmark = pytest.mark.gpu
+
+L1_INIT = np.uint32(0x80)
+
+
+def _check(w, wl, frames, verdict, ref, what):
+    bad = np.nonzero((verdict & ~L1_INIT) != (ref["verdict"] & ~L1_INIT))[0]
+    assert bad.size == 0, f"{what}: {bad.size} verdicts differ, first {bad[:8].tolist()}"
+    assert np.array_equal(frames, ref["frames"]), f"{what}: frames differ"
+    counters, stats = w.get_stats()
+    assert counters.tobytes() == np.asarray(ref["counters"]).tobytes(), what
+    assert np.array_equal(stats, ref["rule_stats"]), what
+    assert w.get_l1().tobytes() == np.asarray(ref["l1"]).tobytes(), what
+
+
+@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "config_d_small"])
+@pytest.mark.parametrize("chunk,pinned", [(1000, True), (333, False), (0, True)])
+def test_host_roundtrip_golden(gpu_worker_factory, case, chunk, pinned):
+    wl, ref = golden_io.load(case)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        if pinned:
+            pf = gpu.PinnedArray(wl.frames.shape, np.uint8)
+            pd = gpu.PinnedArray(wl.desc.shape, np.uint64)
+            pv = gpu.PinnedArray((wl.n,), np.uint32)
+            frames, desc, verdict = pf.array, pd.array, pv.array
+        else:
+            frames, desc, verdict = np.empty_like(wl.frames), np.empty_like(wl.desc), \
+                np.zeros(wl.n, np.uint32)
+        frames[:] = wl.frames
+        desc[:] = wl.desc
+        w.process_host(frames, desc, verdict, chunk)
+        _check(w, wl, frames, verdict, ref, f"{case} chunk={chunk} pinned={pinned}")
+        if pinned:
+            for x in (pf, pd, pv):
+                x.free()
+    finally:
+        w.close()
+
+
+def test_host_roundtrip_header_windows(gpu_worker_factory):
+    """IMIX shipped as 96-byte header windows: same verdicts, counters and rule_stats as the full
+    frames, and the written-back window bytes equal the reference's rewritten frame bytes."""
+    wl, ref = golden_io.load("config_c_small")
+    hw = synth.header_windows(wl)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        frames = hw.frames.copy()
+        verdict = np.zeros(wl.n, np.uint32)
+        w.process_host(frames, hw.desc, verdict, 1500)
+        assert np.array_equal(verdict & ~L1_INIT, ref["verdict"] & ~L1_INIT)
+        counters, stats = w.get_stats()
+        assert counters.tobytes() == np.asarray(ref["counters"]).tobytes()
+        assert np.array_equal(stats, ref["rule_stats"])
+        offs, woffs, lens = desc_offsets(wl.desc), desc_offsets(hw.desc), desc_lens(wl.desc)
+        for i in range(wl.n):
+            k = int(min(lens[i], REWRITE_EXTENT))
+            assert np.array_equal(frames[woffs[i]:woffs[i] + k], ref["frames"][offs[i]:offs[i] + k])
+    finally:
+        w.close()
+
+
+def test_host_roundtrip_full_size_b(gpu_worker_factory):
+    """Config B at 1M through the host path: equals the oracle's sequential run."""
+    wl = synth.config_b()
+    r = oracle.run_restated(wl)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        frames = wl.frames.copy()
+        verdict = np.zeros(wl.n, np.uint32)
+        w.process_host(frames, wl.desc, verdict)
+        _check(w, wl, frames, verdict, {"verdict": r.verdict, "frames": r.frames,
+                                        "counters": r.counters, "rule_stats": r.rule_stats,
+                                        "l1": r.l1}, "B 1M host")
+    finally:
+        w.close()
+
+
+def test_host_roundtrip_rejects_short_buffer(gpu_worker_factory):
+    wl, _ = golden_io.load("config_b_small")
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        verdict = np.zeros(wl.n, np.uint32)
+        with pytest.raises(gpu.UpeGpuError):
+            w.process_host(wl.frames[: int(desc_offsets(wl.desc)[-1]) + 8].copy(), wl.desc, verdict)
+    finally:
+        w.close()

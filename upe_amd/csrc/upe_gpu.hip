@@ -1084,6 +1084,18 @@ struct upe_gpu_ctx {
     uint32_t timing_every = 1, timing_calls = 0;   // sample every n-th process() call
     std::vector<hipEvent_t> ev;   // event pool, 2 per timed process() call
     size_t ev_used = 0;
+    // host round trip (upe_gpu_process_host): copy streams and three device slots
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    struct HostSlot {
+        uint8_t* frames = nullptr;
+        size_t frames_cap = 0;
+        uint64_t* desc = nullptr;
+        uint32_t* verdict = nullptr;
+        size_t pk_cap = 0;
+        hipEvent_t in_done = nullptr, k_done = nullptr, out_done = nullptr;
+        bool busy = false;
+    };
+    HostSlot hs[3];
 };
 
 namespace {
@@ -1275,6 +1287,14 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    for (auto& sl : c->hs) {
+        for (void* b : {(void*)sl.frames, (void*)sl.desc, (void*)sl.verdict})
+            if (b) (void)hipFree(b);
+        for (hipEvent_t e : {sl.in_done, sl.k_done, sl.out_done})
+            if (e) (void)hipEventDestroy(e);
+    }
+    if (c->s_in) (void)hipStreamSynchronize(c->s_in), (void)hipStreamDestroy(c->s_in);
+    if (c->s_out) (void)hipStreamSynchronize(c->s_out), (void)hipStreamDestroy(c->s_out);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1565,6 +1585,110 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(ev[1], s));
     c->have_batch = true;
+    return 0;
+}
+
+int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
+                         const uint64_t* h_desc, uint32_t* h_verdict, size_t n, size_t chunk) {
+    if (!c) return fail("null context");
+    if (n && (!h_frames || !h_desc || !h_verdict)) return fail("null host buffer");
+    HIP_TRY(hipSetDevice(c->device));
+    if (chunk == 0) chunk = (size_t)1 << 18;
+    if (!c->s_in) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+        for (auto& sl : c->hs) {
+            HIP_TRY(hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&sl.k_done, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&sl.out_done, hipEventDisableTiming));
+        }
+    }
+    if (n == 0) {
+        if (upe_gpu_process(c, nullptr, nullptr, nullptr, 0, nullptr) != 0) return -1;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    int rc = 0;
+    size_t k = 0;
+    for (size_t s = 0; s < n && rc == 0; s += chunk, ++k) {
+        const size_t e = n - s < chunk ? n : s + chunk, m = e - s;
+        // The chunk's byte ranges: [lo, hi) holds every frame's window (the kernel reads up to
+        // UPE_FRAME_TAIL bytes from a frame start), [lo, wb) every byte the kernel may rewrite.
+        // The scan of chunk k+1 overlaps the copies and kernel of chunk k.
+        uint64_t lo = ~0ull, hi = 0, wb = 0;
+        for (size_t i = s; i < e; ++i) {
+            const uint64_t off = h_desc[i] >> 16, len = h_desc[i] & 0xFFFFu;
+            if (off & 15u) {
+                rc = fail("frame offsets must be multiples of 16 (include/upe_gpu.h)");
+                break;
+            }
+            lo = off < lo ? off : lo;
+            hi = off + UPE_FRAME_TAIL > hi ? off + UPE_FRAME_TAIL : hi;
+            const uint64_t w = off + (len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT);
+            wb = w > wb ? w : wb;
+        }
+        if (rc) break;
+        if (hi > frames_bytes) {
+            rc = fail("a frame window runs past frames_bytes (UPE_FRAME_TAIL bytes must follow "
+                      "every frame start)");
+            break;
+        }
+        auto& sl = c->hs[k % 3];
+        if (sl.busy) HIP_TRY(hipEventSynchronize(sl.out_done));   // the slot's last D2H is done
+        sl.busy = false;
+        const size_t span = (size_t)(hi - lo);
+        if (span > sl.frames_cap) {
+            if (sl.frames) HIP_TRY(hipFree(sl.frames));
+            sl.frames = nullptr;
+            sl.frames_cap = 0;
+            const size_t want = span + span / 4;
+            HIP_TRY(hipMalloc(&sl.frames, want));
+            sl.frames_cap = want;
+        }
+        if (m > sl.pk_cap) {
+            if (sl.desc) HIP_TRY(hipFree(sl.desc));
+            if (sl.verdict) HIP_TRY(hipFree(sl.verdict));
+            sl.desc = nullptr;
+            sl.verdict = nullptr;
+            sl.pk_cap = 0;
+            HIP_TRY(hipMalloc(&sl.desc, m * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&sl.verdict, m * sizeof(uint32_t)));
+            sl.pk_cap = m;
+        }
+        HIP_TRY(hipMemcpyAsync(sl.frames, h_frames + lo, span, hipMemcpyHostToDevice, c->s_in));
+        HIP_TRY(hipMemcpyAsync(sl.desc, h_desc + s, m * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               c->s_in));
+        HIP_TRY(hipEventRecord(sl.in_done, c->s_in));
+        HIP_TRY(hipStreamWaitEvent(c->stream, sl.in_done, 0));
+        // the descriptors keep their offsets relative to h_frames: hand the kernel a base that
+        // maps offset lo onto the slot (lo is a multiple of 16, so the base stays aligned)
+        uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.frames) - lo);
+        if (upe_gpu_process(c, base, sl.desc, sl.verdict, m, nullptr) != 0) return -1;
+        HIP_TRY(hipEventRecord(sl.k_done, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->s_out, sl.k_done, 0));
+        HIP_TRY(hipMemcpyAsync(h_verdict + s, sl.verdict, m * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, c->s_out));
+        HIP_TRY(hipMemcpyAsync(h_frames + lo, sl.frames, (size_t)(wb - lo), hipMemcpyDeviceToHost,
+                               c->s_out));
+        HIP_TRY(hipEventRecord(sl.out_done, c->s_out));
+        sl.busy = true;
+    }
+    HIP_TRY(hipStreamSynchronize(c->s_out));
+    for (auto& sl : c->hs) sl.busy = false;
+    return rc;
+}
+
+void* upe_gpu_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        fail("hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int upe_gpu_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
     return 0;
 }
 

@@ -54,6 +54,9 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_free": (I, [P, P]),
         "upe_gpu_memcpy_h2d": (I, [P, P, P, SZ, P]),
         "upe_gpu_memcpy_d2h": (I, [P, P, P, SZ, P]),
+        "upe_gpu_process_host": (I, [P, P, SZ, P, P, SZ, SZ]),
+        "upe_gpu_host_alloc": (P, [SZ]),
+        "upe_gpu_host_free": (I, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -70,7 +73,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
-            "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h")
+            "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
+            "upe_gpu_host_alloc", "upe_gpu_host_free")
 
 
 def _check(rc: int, what: str) -> None:
@@ -193,6 +197,18 @@ class GpuWorker:
                                        ctypes.byref(n)), "upe_gpu_timing_read")
         return a.value, b.value, n.value
 
+    # ---- host round trip (pinned host batch in, verdicts and rewritten headers out) ----
+    def process_host(self, frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray,
+                     chunk: int = 0) -> None:
+        """upe_gpu_process_host over host arrays (frames rewritten in place)."""
+        assert frames.dtype == np.uint8 and desc.dtype == np.uint64 and verdict.dtype == np.uint32
+        assert verdict.shape[0] >= desc.shape[0]
+        _check(LIB.upe_gpu_process_host(self._ctx, _np_ptr(frames), frames.nbytes,
+                                        _np_ptr(desc) if desc.size else None,
+                                        _np_ptr(verdict) if verdict.size else None,
+                                        int(desc.shape[0]), int(chunk)),
+               "upe_gpu_process_host")
+
     # ---- device memory without torch ----
     def malloc(self, nbytes: int) -> int:
         p = LIB.upe_gpu_malloc(self._ctx, nbytes)
@@ -210,6 +226,25 @@ class GpuWorker:
     def d2h(self, host: np.ndarray, dptr: int, stream=None) -> None:
         _check(LIB.upe_gpu_memcpy_d2h(self._ctx, _np_ptr(host), dptr, host.nbytes, stream or None),
                "upe_gpu_memcpy_d2h")
+
+
+class PinnedArray:
+    """A numpy view of page-locked host memory (upe_gpu_host_alloc); freed by free()."""
+
+    def __init__(self, shape, dtype):
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dtype.itemsize
+        self.ptr = LIB.upe_gpu_host_alloc(max(nbytes, 1))
+        if not self.ptr:
+            raise UpeGpuError(f"upe_gpu_host_alloc: {LIB.upe_gpu_last_error().decode()}")
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(self.ptr)
+        self.array = np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            LIB.upe_gpu_host_free(self.ptr)
+            self.ptr = None
 
 
 class DeviceBatch:

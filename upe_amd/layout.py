@@ -65,6 +65,7 @@ ACT_DROP, ACT_FWD = 0, 1
 
 HDR_WINDOW = 96
 FRAME_TAIL = 96
+REWRITE_EXTENT = 48
 
 
 def verdict_code(v: np.ndarray) -> np.ndarray:

@@ -17,8 +17,8 @@ import dataclasses
 
 import numpy as np
 
-from .layout import (ACT_DROP, ACT_FWD, ARP_DTYPE, FRAME_TAIL, NDP_DTYPE, RULE_DTYPE,
-                     l1_zero, make_desc)
+from .layout import (ACT_DROP, ACT_FWD, ARP_DTYPE, FRAME_TAIL, HDR_WINDOW, NDP_DTYPE,
+                     RULE_DTYPE, desc_lens, desc_offsets, l1_zero, make_desc)
 
 PORT_MAC = bytes([0x02, 0x00, 0x00, 0x00, 0x00, 0x01])
 PORT_IP4 = 0x0A8000FE  # 10.128.0.254
@@ -600,6 +600,29 @@ def config_d(n: int = 1 << 24, seed: int = 4, n_rules: int = 1 << 16) -> Workloa
             lens[rows] = np.where(h[rows, 12] == 0x08, np.minimum(lens[rows], 60), lens[rows])
     frames, desc = pack_frames(h, lens, stride=128)
     return Workload("D", frames, desc, rules, n_rules, arp, ndp)
+
+
+def header_windows(wl: Workload, window: int = HDR_WINDOW) -> Workload:
+    """The same packets as header windows: frame i becomes its first min(len, window) bytes at
+    offset i * window (descriptor lengths stay the real lengths, so rule_stats bytes are
+    unchanged).  What a host-side batch builder ships instead of whole frames: the path reads at
+    most UPE_HDR_WINDOW bytes of a frame and rewrites at most UPE_REWRITE_EXTENT."""
+    offs = desc_offsets(wl.desc)
+    lens = desc_lens(wl.desc)
+    n = wl.n
+    out = np.zeros(n * window + FRAME_TAIL + 128, dtype=np.uint8)
+    cols = np.arange(window)
+    chunk = 1 << 16
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        keep = np.minimum(lens[s:e], window)
+        m = cols[None, :] < keep[:, None]
+        src = offs[s:e, None] + cols[None, :]
+        dst = (np.arange(s, e, dtype=np.int64) * window)[:, None] + cols[None, :]
+        out[dst[m]] = wl.frames[src[m]]
+    desc = make_desc(np.arange(n, dtype=np.int64) * window, lens)
+    return dataclasses.replace(wl, frames=out, desc=desc, arp=wl.arp.copy(), ndp=wl.ndp.copy(),
+                               l1=wl.l1.copy())
 
 
 CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d}
