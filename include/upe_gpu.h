@@ -191,6 +191,12 @@ void upe_gpu_close(upe_gpu_ctx_t *ctx);
  * w->rt (src/worker.c:129).  count <= rule capacity given at open, every rule_id < capacity. */
 int upe_gpu_load_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count);
 
+/* How the loaded table is classified: 0 = linear first-match scan (small tables, or many mask
+ * signatures), 1 = tuple-space index (large tables whose rules fall into few mask signatures:
+ * one hash probe per signature, visited in order of each signature's first rule, so the result
+ * is still the first match in (priority, rule_id) order).  -1 on error. */
+int upe_gpu_rule_index_kind(upe_gpu_ctx_t *ctx);
+
 /* Upload a snapshot of the neighbour tables' slot arrays (arpt->entries / ndpt->entries with
  * their power-of-two capacities).  Lookups probe exactly as arp_get_mac/ndp_get_mac do.
  * Either table may be NULL with capacity 0 (every lookup misses). */

@@ -258,3 +258,37 @@ def test_lookback_far_first_hit(gpu_worker_factory, first_hit):
     got = _run(gpu_worker_factory, wl)
     _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                        "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
+                                  "config_d_small", "edge_inconsistent"])
+def test_rule_index_kinds_agree(gpu_worker_factory, monkeypatch, case, mode):
+    """Both classifiers — the linear first-match scan and the tuple-space index — forced on
+    every fixture (version-0 rules, mixed v4/v6 masks, wildcard fields, catch-alls) give the
+    reference's first match."""
+    monkeypatch.setenv("UPE_GPU_TSS", mode)
+    wl, ref = golden_io.load(case)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        assert w.rule_index_kind() == int(mode)
+        frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w)
+    finally:
+        w.close()
+    if case.startswith("edge"):
+        # one segment (control writes deferred): compare with the oracle run the same way
+        r = oracle.run_restated(wl, apply_control=False)
+        ref = {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
+               "rule_stats": r.rule_stats, "l1": r.l1}
+    _assert_same((frames, verdict, counters, stats, l1), ref, f"{case} tss={mode}")
+
+
+def test_config_d_uses_tuple_space(gpu_worker_factory):
+    wl, _ = golden_io.load("config_d_small")
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        assert w.rule_index_kind() == 1
+    finally:
+        w.close()

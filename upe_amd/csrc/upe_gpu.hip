@@ -54,7 +54,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <array>
+#include <map>
 #include <new>
 #include <string>
 #include <vector>
@@ -178,6 +180,19 @@ struct NeighIndex {
     uint32_t seed;
 };
 
+// Tuple-space index of a large rule table (built by upe_gpu_load_rules when it pays): the rules
+// a packet family can match are grouped by mask signature; a group's cuckoo table maps the
+// masked key to the smallest sorted index with that key.  Group descriptor words:
+//   [0] m0 (proto, src_port masks)  [1] m1 (dst_port mask)  [2] src word-0 mask
+//   [3] dst word-0 mask  [4..6] src words 1-3 masks  [7..9] dst words 1-3 masks (family 6)
+//   [10] smallest sorted index in the group  [11] log2(slots)  [12] seed  [13] first slot
+// Slots: family 4 = 2 x uint4 {k0, k1, s0, d0}, {index, used, -, -};
+//        family 6 = 3 x uint4 {k0, k1, s0, s1}, {s2, s3, d0, d1}, {d2, d3, index, used}.
+struct __attribute__((aligned(16))) TssGroup {
+    uint32_t w[16];
+};
+constexpr int kTssSlot4 = 2, kTssSlot6 = 3;   // uint4 per slot
+
 struct Args {
     uint8_t* frames;
     const uint64_t* desc;
@@ -191,6 +206,12 @@ struct Args {
     uint32_t port_mac_lo, port_mac_hi, port_ip4;
     NeighIndex arp, ndp;
     DevState* st;
+    // tuple-space index (tss != 0): replaces the linear scan for large tables
+    const TssGroup* tg4;
+    const TssGroup* tg6;
+    const uint4* tt4;
+    const uint4* tt6;
+    uint32_t ng4, ng6, tss;
 };
 
 // ---- small helpers ------------------------------------------------------------------------
@@ -323,6 +344,78 @@ __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is
         if (__all(done)) break;
     }
     return hit;
+}
+
+// Key hash of the tuple-space index (host and device agree bit for bit).
+__host__ __device__ __forceinline__ uint32_t tss_hash(const uint32_t* k, int nw, uint32_t seed) {
+    uint32_t h = seed ^ 0x9E3779B9u;
+    for (int j = 0; j < nw; ++j) {
+        h = (h ^ k[j]) * 0x01000193u;
+        h ^= h >> 15;
+    }
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// First match through the tuple-space index for one packet family (F = 4 or 6).  Groups are
+// visited in order of their smallest sorted index, so once a lane's best index is below the
+// next group's smallest, nothing later can precede it: the result is exactly the first match
+// of the linear scan (reference src/rule_table.c:163-176).
+template <int F>
+__device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32_t k0, uint32_t k1,
+                                              const uint32_t s[4], const uint32_t d[4]) {
+    uint32_t best = kNone;
+    const uint32_t ng = F == 4 ? a.ng4 : a.ng6;
+    const auto* G = as_const<u32x16>(F == 4 ? a.tg4 : a.tg6);
+    const uint4* T = F == 4 ? a.tt4 : a.tt6;
+    for (uint32_t g = 0; g < ng; ++g) {
+        const u32x16 q = G[__builtin_amdgcn_readfirstlane(g)];
+        const bool want = active && best > q[10];
+        if (!__any(want)) break;
+        if (want) {
+            constexpr int nw = F == 4 ? 4 : 10;
+            uint32_t kw[nw];
+            kw[0] = k0 & q[0];
+            kw[1] = k1 & q[1];
+            kw[2] = s[0] & q[2];
+            if constexpr (F == 4) {
+                kw[3] = d[0] & q[3];
+            } else {
+                kw[3] = s[1] & q[4]; kw[4] = s[2] & q[5]; kw[5] = s[3] & q[6];
+                kw[6] = d[0] & q[3];
+                kw[7] = d[1] & q[7]; kw[8] = d[2] & q[8]; kw[9] = d[3] & q[9];
+            }
+            const uint32_t h = tss_hash(kw, nw, q[12]);
+            const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
+            const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
+            uint32_t idx = kNone;
+            if constexpr (F == 4) {
+                const uint4 a1 = T[2 * t1], b1 = T[2 * t1 + 1];
+                const uint4 a2 = T[2 * t2], b2 = T[2 * t2 + 1];
+                const bool h1 = b1.y && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
+                                a1.w == kw[3];
+                const bool h2 = b2.y && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
+                                a2.w == kw[3];
+                idx = h1 ? b1.x : h2 ? b2.x : kNone;
+            } else {
+                const uint4 a1 = T[3 * t1], b1 = T[3 * t1 + 1], c1 = T[3 * t1 + 2];
+                const uint4 a2 = T[3 * t2], b2 = T[3 * t2 + 1], c2 = T[3 * t2 + 2];
+                const bool h1 = c1.w && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
+                                a1.w == kw[3] && b1.x == kw[4] && b1.y == kw[5] &&
+                                b1.z == kw[6] && b1.w == kw[7] && c1.x == kw[8] && c1.y == kw[9];
+                const bool h2 = c2.w && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
+                                a2.w == kw[3] && b2.x == kw[4] && b2.y == kw[5] &&
+                                b2.z == kw[6] && b2.w == kw[7] && c2.x == kw[8] && c2.y == kw[9];
+                idx = h1 ? c1.z : h2 ? c2.z : kNone;
+            }
+            best = min(best, idx);
+        }
+    }
+    return best;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -649,6 +742,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
 // ------------------------------------------------------------------------------------------
 // classify: persistent workgroups over 256-packet tiles
 // ------------------------------------------------------------------------------------------
+template <bool kTssMode>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     __shared__ uint32_t s_cnt[C_N];
@@ -814,9 +908,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint32_t k0 = (r.v6 ? 6u : 4u) | (r.proto << 8) | (r.sport << 16);
         const uint32_t k1 = r.dport;
         const bool need_v6 = __any(ok && r.v6);
-        const uint32_t ri = (kAblate & 1) ? (ok ? 0u : kNone)
-                            : need_v6 ? scan_rules<true>(a, !ok, r.v6, k0, k1, r.s, r.d)
-                                      : scan_rules<false>(a, !ok, r.v6, k0, k1, r.s, r.d);
+        uint32_t ri;
+        if (kAblate & 1) {
+            ri = ok ? 0u : kNone;
+        } else if (kTssMode) {
+            const uint32_t r4 = tss_match<4>(a, ok && !r.v6, k0, k1, r.s, r.d);
+            const uint32_t r6 = need_v6 ? tss_match<6>(a, ok && r.v6, k0, k1, r.s, r.d) : kNone;
+            ri = r.v6 ? r6 : r4;
+        } else {
+            ri = need_v6 ? scan_rules<true>(a, !ok, r.v6, k0, k1, r.s, r.d)
+                         : scan_rules<false>(a, !ok, r.v6, k0, k1, r.s, r.d);
+        }
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
         uint32_t code = 0, rbits = 0;
@@ -1056,6 +1158,13 @@ struct upe_gpu_ctx {
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
     std::vector<int2> rinfo_host;              // (action, rule_id) per sorted index
+    // tuple-space index of large tables (null when the linear scan is used)
+    TssGroup* tg4 = nullptr;
+    TssGroup* tg6 = nullptr;
+    uint4* tt4 = nullptr;
+    uint4* tt6 = nullptr;
+    uint32_t ng4 = 0, ng6 = 0;
+    bool tss = false;
     // neighbour tables (reachable-entry indexes)
     uint4* arp = nullptr;
     uint32_t arp_bits = 0, arp_seed = 0;
@@ -1076,6 +1185,7 @@ struct upe_gpu_ctx {
     int cus = 256;
     uint32_t resident = 0;         // persistent grid size for resident_lds bytes of dynamic LDS
     size_t resident_lds = 0;
+    bool resident_tss = false;
     int blocks_per_cu_override = 0;   // UPE_GPU_BLOCKS_PER_CU (diagnostic)
     uint32_t port_mac_lo = 0, port_mac_hi = 0, port_ip4 = 0;
     bool have_batch = false;
@@ -1106,9 +1216,19 @@ NeighIndex ndp_index(const upe_gpu_ctx* c) { return NeighIndex{c->ndp, c->ndp_bi
 // Two-choice cuckoo placement of distinct keys (by their 32-bit hash key; different entries may
 // share a hash key, the device compares the full address).  Starts at 2^bits >= 2.5 n slots and
 // tries seeds, then doubles, until every key sits in slot1 or slot2.  bits = 0 for no keys.
+template <class H>
+int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot);
+
 int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& seed,
                  std::vector<int32_t>& slot) {
-    const size_t n = key.size();
+    return cuckoo_place_fn(key.size(), [&](size_t j, uint32_t) { return key[j]; }, bits, seed,
+                           slot);
+}
+
+// Same, with a seed-dependent 32-bit hash per key: hfn(j, seed).
+template <class H>
+int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot) {
+    std::vector<uint32_t> key(n);
     slot.clear();
     bits = 0;
     seed = 0;
@@ -1119,6 +1239,7 @@ int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& see
         const size_t m = (size_t)1 << bits;
         for (uint32_t attempt = 0; attempt < 64; ++attempt) {
             const uint32_t sd = attempt * 0x6D2B79F5u + bits;
+            for (size_t j = 0; j < n; ++j) key[j] = hfn(j, sd);
             slot.assign(m, -1);
             bool ok = true;
             for (size_t j = 0; j < n && ok; ++j) {
@@ -1283,7 +1404,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->cand_tile};
+                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1322,6 +1443,121 @@ int fold_stats_idx(upe_gpu_ctx* c) {
     return 0;
 }
 }  // namespace
+
+}  // extern "C"
+
+namespace {
+// Tuple-space index of the compiled rules (see TssGroup).  Returns false when the table is
+// better served by the linear scan: small tables, or too many distinct mask signatures.
+struct TssFamily {
+    std::vector<TssGroup> groups;
+    std::vector<uint4> slots;
+};
+
+bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                      const upe_rule_t* rules, size_t count, TssFamily& out) {
+    const int nw = F == 4 ? 4 : 10;
+    using Sig = std::array<uint32_t, 10>;
+    using Key = std::array<uint32_t, 10>;
+    struct Grp {
+        uint32_t minidx = kNone;
+        std::map<Key, uint32_t> keys;   // masked key -> smallest sorted index
+    };
+    std::map<Sig, Grp> groups;
+    for (size_t i = 0; i < count; ++i) {
+        const uint8_t ver = rules[i].ip_ver;
+        if (ver != 0 && ver != F) continue;
+        const RuleV4& r = v4[i];
+        const RuleV6& q = v6[i];
+        Sig sg{};
+        Key k{};
+        sg[0] = r.m0 & ~0xFFu;
+        sg[1] = r.m1 & 0xFFFFu;
+        sg[2] = r.sm0;
+        sg[3] = r.dm0;
+        k[0] = r.x0 & sg[0];
+        k[1] = r.x1 & sg[1];
+        k[2] = r.s0;
+        if (F == 4) {
+            k[3] = r.d0;
+        } else {
+            for (int j = 0; j < 3; ++j) {
+                sg[4 + j] = q.sm[j];
+                sg[7 + j] = q.dm[j];
+            }
+            k[3] = q.s[0]; k[4] = q.s[1]; k[5] = q.s[2];
+            k[6] = r.d0;
+            k[7] = q.d[0]; k[8] = q.d[1]; k[9] = q.d[2];
+        }
+        Grp& g = groups[sg];
+        if (g.minidx == kNone) g.minidx = (uint32_t)i;
+        g.keys.emplace(k, (uint32_t)i);   // first insertion = smallest sorted index
+    }
+    std::vector<std::pair<uint32_t, const std::pair<const Sig, Grp>*>> order;
+    for (const auto& kv : groups) order.push_back({kv.second.minidx, &kv});
+    std::sort(order.begin(), order.end(),
+              [](const auto& x, const auto& y) { return x.first < y.first; });
+    const int per = F == 4 ? kTssSlot4 : kTssSlot6;
+    out.groups.clear();
+    out.slots.clear();
+    for (const auto& o : order) {
+        const Sig& sg = o.second->first;
+        const Grp& g = o.second->second;
+        std::vector<Key> keys;
+        std::vector<uint32_t> idx;
+        for (const auto& kv : g.keys) {
+            keys.push_back(kv.first);
+            idx.push_back(kv.second);
+        }
+        uint32_t bits = 0, seed = 0;
+        std::vector<int32_t> slot;
+        if (cuckoo_place_fn(keys.size(),
+                            [&](size_t j, uint32_t sd) { return tss_hash(keys[j].data(), nw, sd); },
+                            bits, seed, slot) != 0)
+            return false;
+        TssGroup d;
+        memset(&d, 0, sizeof d);
+        for (int j = 0; j < 10; ++j) d.w[j] = sg[j];
+        d.w[10] = g.minidx;
+        d.w[11] = bits;
+        d.w[12] = seed;
+        d.w[13] = (uint32_t)(out.slots.size() / per);
+        out.groups.push_back(d);
+        const size_t base = out.slots.size();
+        out.slots.resize(base + slot.size() * per, make_uint4(0, 0, 0, 0));
+        for (size_t t = 0; t < slot.size(); ++t) {
+            if (slot[t] < 0) continue;
+            const Key& k = keys[slot[t]];
+            uint4* e = &out.slots[base + t * per];
+            if (F == 4) {
+                e[0] = make_uint4(k[0], k[1], k[2], k[3]);
+                e[1] = make_uint4(idx[slot[t]], 1u, 0u, 0u);
+            } else {
+                e[0] = make_uint4(k[0], k[1], k[2], k[3]);
+                e[1] = make_uint4(k[4], k[5], k[6], k[7]);
+                e[2] = make_uint4(k[8], k[9], idx[slot[t]], 1u);
+            }
+        }
+    }
+    return true;
+}
+
+int upload_bytes(void** dst, const void* src, size_t bytes) {
+    if (*dst) (void)hipFree(*dst);
+    *dst = nullptr;
+    if (bytes == 0) return 0;
+    HIP_TRY(hipMalloc(dst, bytes));
+    HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+int upload(TssGroup*& dst, const std::vector<TssGroup>& v) {
+    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(TssGroup));
+}
+int upload(uint4*& dst, const std::vector<uint4>& v) {
+    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint4));
+}
+}  // namespace
+extern "C" {
 
 extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count) {
     if (!c) return fail("null context");
@@ -1394,7 +1630,33 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     c->nrules = (uint32_t)count;
     c->nrules_pad = (uint32_t)pad;
     c->rinfo_host = info;
+
+    // Large tables: a tuple-space index when the rules fall into few mask signatures (one hash
+    // probe per signature instead of a test per rule); otherwise the linear scan.
+    c->tss = false;
+    c->ng4 = c->ng6 = 0;
+    const char* force = getenv("UPE_GPU_TSS");   // diagnostic: 0 = never, 1 = always
+    if (count > 0 && !(force && force[0] == '0')) {
+        TssFamily f4, f6;
+        if (build_tss_family(4, v4, v6, rules, count, f4) &&
+            build_tss_family(6, v4, v6, rules, count, f6)) {
+            const size_t ng = f4.groups.size() + f6.groups.size();
+            if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
+                if (upload(c->tg4, f4.groups) || upload(c->tg6, f6.groups) ||
+                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots))
+                    return -1;
+                c->ng4 = (uint32_t)f4.groups.size();
+                c->ng6 = (uint32_t)f6.groups.size();
+                c->tss = true;
+            }
+        }
+    }
     return 0;
+}
+
+extern "C" int upe_gpu_rule_index_kind(upe_gpu_ctx_t* c) {
+    if (!c) return fail("null context");
+    return c->tss ? 1 : 0;
 }
 
 int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_capacity,
@@ -1569,19 +1831,31 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     a.port_mac_lo = c->port_mac_lo;
     a.port_mac_hi = c->port_mac_hi;
     a.port_ip4 = c->port_ip4;
+    a.tg4 = c->tg4;
+    a.tg6 = c->tg6;
+    a.tt4 = c->tt4;
+    a.tt6 = c->tt6;
+    a.ng4 = c->ng4;
+    a.ng6 = c->ng6;
+    a.tss = c->tss ? 1u : 0u;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     const size_t lds = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
-    if (c->resident_lds != lds || c->resident == 0) {
+    if (c->resident_lds != lds || c->resident == 0 || c->resident_tss != c->tss) {
+        c->resident_tss = c->tss;
         int per_cu = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify, kBlock, lds));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, c->tss ? upe_classify<true> : upe_classify<false>, kBlock, lds));
         if (per_cu < 1) per_cu = 1;
         if (c->blocks_per_cu_override > 0) per_cu = c->blocks_per_cu_override;
         c->resident = (uint32_t)per_cu * (uint32_t)c->cus;
         c->resident_lds = lds;
     }
     const uint32_t grid = ntiles == 0 ? 1u : ntiles < c->resident ? ntiles : c->resident;
-    hipLaunchKernelGGL(upe_classify, dim3(grid), dim3(kBlock), lds, s, a);
+    if (c->tss)
+        hipLaunchKernelGGL(upe_classify<true>, dim3(grid), dim3(kBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL(upe_classify<false>, dim3(grid), dim3(kBlock), lds, s, a);
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(ev[1], s));
     c->have_batch = true;

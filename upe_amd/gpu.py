@@ -40,6 +40,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_close": (None, [P]),
         "upe_gpu_load_rules": (I, [P, P, SZ]),
         "upe_gpu_load_neigh": (I, [P, P, SZ, P, SZ]),
+        "upe_gpu_rule_index_kind": (I, [P]),
         "upe_gpu_set_port": (I, [P, P, ctypes.c_uint32]),
         "upe_gpu_set_l1": (I, [P, P]),
         "upe_gpu_get_l1": (I, [P, P]),
@@ -69,7 +70,7 @@ LIB = _load()
 
 # every symbol include/upe_gpu.h declares (checked by tests/test_abi.py)
 EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_gpu_close",
-            "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_set_port", "upe_gpu_set_l1",
+            "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
             "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
@@ -132,6 +133,13 @@ class GpuWorker:
         r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
         _check(LIB.upe_gpu_load_rules(self._ctx, _np_ptr(r) if len(r) else None, len(r)),
                "upe_gpu_load_rules")
+
+    def rule_index_kind(self) -> int:
+        """0: linear scan, 1: tuple-space index."""
+        k = LIB.upe_gpu_rule_index_kind(self._ctx)
+        if k < 0:
+            raise UpeGpuError(LIB.upe_gpu_last_error().decode())
+        return k
 
     def load_neigh(self, arp: np.ndarray | None, ndp: np.ndarray | None) -> None:
         a = np.ascontiguousarray(arp if arp is not None else np.zeros(0, ARP_DTYPE), ARP_DTYPE)
