@@ -1,0 +1,1 @@
+bash tools/gpu_session.sh "varD:600:bash tools/variants_d.sh"

@@ -931,12 +931,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else {
             const int2 info = a.rinfo[ri];
             rbits = (ri + 1) << 8;
-            // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: LDS histogram below for
-            // LDS-resident tables, direct device atomics for very large ones
-            if (!(kAblate & 4) && !lds_stats) {
-                atomicAdd(&a.st->stats[2 * (uint32_t)info.y], 1ull);
-                atomicAdd(&a.st->stats[2 * (uint32_t)info.y + 1], (unsigned long long)len);
-            }
+            // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: an LDS histogram below for
+            // LDS-resident tables; for larger ones upe_rule_hist folds the verdict words after
+            // the launch (one scattered device atomic per packet would cost more than the
+            // whole classification)
             code = info.x == UPE_ACT_DROP ? UPE_V_DROP_RULE
                  : info.x == UPE_ACT_FWD  ? UPE_V_FWD
                                           : UPE_V_DROP_ACTION;
@@ -1120,6 +1118,58 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     batch_tail(a, tid, look4, look6);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// rule_stats of large tables (more rules than an LDS histogram holds): a group-by of the
+// batch's verdict words by matched rule.  Workgroup (x, y) counts the packets of chunk x whose
+// rule falls in range y in LDS, then adds its nonzero bins to the per-sorted-index totals with
+// contiguous device atomics (credited to rule_id on the host, like small tables).  u32 bins
+// cannot overflow: a chunk holds at most 65536 packets of at most 65535 bytes.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kHistRange = 8192;    // rules per workgroup: 64 KB of LDS
+constexpr uint32_t kHistChunk = 65536;   // packets per workgroup
+
+__global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint64_t* desc,
+                                                     uint32_t n, uint32_t nrules,
+                                                     unsigned long long* stats_idx) {
+    // one 64-bit bin per rule: packets << 32 | bytes (a chunk holds at most 65536 packets of
+    // at most 65535 bytes, so neither half overflows)
+    __shared__ unsigned long long h[kHistRange];
+    const uint32_t r0 = blockIdx.y * kHistRange;
+    const uint32_t p0 = blockIdx.x * kHistChunk;
+    for (uint32_t k = threadIdx.x; k < kHistRange; k += 256) h[k] = 0;
+    __syncthreads();
+    const uint32_t pend = n - p0 < kHistChunk ? n : p0 + kHistChunk;
+    // four verdict words per thread per round, loaded together
+    for (uint32_t i = p0 + 4 * threadIdx.x; i < pend; i += 4 * 256) {
+        uint32_t v[4];
+        if (i + 4 <= pend && (i & 3) == 0) {
+            const uint4 q = *reinterpret_cast<const uint4*>(verdict + i);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = i + j < pend ? verdict[i + j] : 0u;
+        }
+        uint32_t len[4];
+        bool in[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
+            in[j] = rb != 0 && rb - 1u - r0 < kHistRange;
+            len[j] = in[j] ? (uint32_t)(desc[i + j] & 0xFFFFu) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (in[j]) atomicAdd(&h[(v[j] >> 8) - 1u - r0], (1ull << 32) | len[j]);
+    }
+    __syncthreads();
+    const uint32_t rend = nrules - r0 < kHistRange ? nrules : r0 + kHistRange;
+    for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
+        const unsigned long long b = h[k >> 1];
+        const unsigned long long x = (k & 1) ? (b & 0xFFFFFFFFull) : (b >> 32);
+        if (x) atomicAdd(&stats_idx[2 * (size_t)r0 + k], x);
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // host side
@@ -1424,8 +1474,14 @@ namespace {
 // Credit the sorted-index totals of the current table to rule_stats[rule_id] (device) and clear
 // them: called before the table changes, so a reload keeps every count (src/main.c:216-282
 // swaps rule_stats with the table; here the counts simply carry over by rule_id).
+// Tables whose counts are kept per sorted index (credited to rule_id on the host): small ones
+// (replicated accumulators) and large ones (upe_rule_hist); mid-size ones go straight to rule_id.
+bool idx_stats(const upe_gpu_ctx* c) {
+    return c->nrules_pad <= (uint32_t)kSmallRules || c->nrules_pad > (uint32_t)kLdsStatsMax;
+}
+
 int fold_stats_idx(upe_gpu_ctx* c) {
-    if (!c->stats_idx || c->rinfo_host.empty() || c->nrules_pad > (uint32_t)kSmallRules) return 0;
+    if (!c->stats_idx || c->rinfo_host.empty() || !idx_stats(c)) return 0;
     const size_t E = 2 * (size_t)c->nrules_pad;
     std::vector<unsigned long long> idx(E), st(2 * c->cap);
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1857,6 +1913,13 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     else
         hipLaunchKernelGGL(upe_classify<false>, dim3(grid), dim3(kBlock), lds, s, a);
     HIP_TRY(hipGetLastError());
+    if (!lds_stats && n > 0 && !(kAblate & 4)) {
+        const dim3 hg((uint32_t)((n + kHistChunk - 1) / kHistChunk),
+                      (c->nrules_pad + kHistRange - 1) / kHistRange);
+        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), 0, s, d_verdict, d_desc, (uint32_t)n,
+                           c->nrules_pad, c->stats_idx);
+        HIP_TRY(hipGetLastError());
+    }
     if (timed) HIP_TRY(hipEventRecord(ev[1], s));
     c->have_batch = true;
     return 0;
@@ -2006,7 +2069,7 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
     if (rule_stats) {
         const size_t k = capacity < c->cap ? capacity : c->cap;
         HIP_TRY(hipMemcpy(rule_stats, c->stats, k * sizeof(upe_rule_stat_t), hipMemcpyDeviceToHost));
-        if (c->nrules_pad <= (uint32_t)kSmallRules && c->stats_idx) {
+        if (idx_stats(c) && c->stats_idx) {
             // small tables keep this table's counts per sorted index: credit them to rule_id
             const size_t E = 2 * (size_t)c->nrules_pad;
             std::vector<unsigned long long> idx(E);
