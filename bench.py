@@ -187,11 +187,12 @@ def main() -> None:
     base = pool.data_ptr()
     torch.cuda.synchronize(dev)
 
-    def step(k: int) -> None:
-        worker.process(base + (k % copies) * stride, desc, verdict, n, sh)
+    def steps(k0: int, count: int) -> None:
+        # queued from native code (upe_gpu_process_batches): no Python round trip per batch
+        worker.process_batches([base + (k % copies) * stride for k in range(k0, k0 + count)],
+                               desc, verdict, n, sh)
 
-    for k in range(args.warmup):
-        step(k)
+    steps(0, args.warmup)
     torch.cuda.synchronize(dev)
     v_first = verdict.cpu().numpy().view(np.uint32).copy()  # warm-up batch 0 verdicts
 
@@ -204,8 +205,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    steps(args.warmup, args.steps)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()

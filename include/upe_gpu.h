@@ -240,6 +240,15 @@ int upe_gpu_process_host(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_by
 void *upe_gpu_host_alloc(size_t bytes);
 int upe_gpu_host_free(void *ptr);
 
+/* Queue `count` batches back to back from native code: batch k is d_frames_list[k] (a host
+ * array of device pointers), all sharing one descriptor array and one verdict array (each batch
+ * overwrites the verdicts of the one before).  Equivalent to `count` upe_gpu_process() calls,
+ * without a caller round trip per batch; what a GPU-backed worker thread does with a ring of
+ * resident batch buffers. */
+int upe_gpu_process_batches(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
+                            const uint64_t *d_desc, uint32_t *d_verdict, size_t n, size_t count,
+                            void *stream);
+
 /* Wait for all work queued on the context's stream (or `stream`). */
 int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
 

@@ -1,0 +1,3 @@
+bash tools/gpu_session.sh \
+ "stamps256k:200:UPE_GPU_LIB_DIAG=$PWD/build/diag/libupe_gpu_stamps.so python tools/stamps.py 262144" \
+ "stamps1M:200:UPE_GPU_LIB_DIAG=$PWD/build/diag/libupe_gpu_stamps.so python tools/stamps.py 1048576"

@@ -1,0 +1,45 @@
+"""Diagnostic: per-workgroup phase timestamps of one upe_classify launch (UPE_STAMPS build).
+Usage: UPE_GPU_LIB_DIAG=build/diag/libupe_gpu_stamps.so python tools/stamps.py [packets]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from upe_amd import gpu, synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+wl = synth.config_b(n=n)
+w = gpu.GpuWorker(0, wl.capacity)
+w.configure(wl)
+dev = torch.device("cuda", 0)
+frames = [torch.from_numpy(wl.frames).to(dev) for _ in range(4)]
+desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+verdict = torch.empty(n, dtype=torch.int32, device=dev)
+lib = gpu.LIB
+lib.upe_gpu_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+names = ["entry", "init", "win", "scan", "loop", "flush", "wait", "ticket", "tail", "reduced", "barrier"]
+for rep in range(4):
+    buf = np.zeros(8192 * 16, np.uint64)
+    lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), 0)  # no-op read
+    w.process(frames[rep], desc, verdict, n)
+    w.sync()
+    lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes)
+    ntiles = (n + 255) // 256
+    grid = min(ntiles, 8192)
+    st = buf.reshape(8192, 16)[:grid, :11].astype(np.int64)
+    valid = st[:, 0] > 0
+    st = st[valid]
+    t0 = st[:, 0].min()
+    rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
+    print(f"rep {rep}: grid {st.shape[0]} WGs; end of kernel ~{rel[:, 7].max():.2f} us; tail end "
+          f"{rel[:, 8].max():.2f} us")
+    for j, nm in enumerate(names):
+        col = rel[:, j]
+        col = col[col >= 0]
+        if j == 8:
+            col = rel[:, 8][st[:, 8] > 0]
+        if col.size:
+            print(f"   {nm:7s} min {col.min():7.2f} med {np.median(col):7.2f} max {col.max():7.2f}")

@@ -72,12 +72,13 @@ constexpr int kBlock = UPE_BLOCK;      // threads per workgroup = packets per ti
 constexpr int kWaves = kBlock / 64;
 constexpr int kTile = kBlock;
 #ifndef UPE_WAVES_PER_SIMD
-#define UPE_WAVES_PER_SIMD 8
+#define UPE_WAVES_PER_SIMD 5
 #endif
 constexpr int kWavesPerSimd = UPE_WAVES_PER_SIMD;   // 8 -> VGPR budget 64
 constexpr int kUnroll = 4;             // rules per early-exit check (rule table padding unit)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kLdsStatsMax = 4096;     // rule_stats histogrammed in LDS up to this many rules
+constexpr uint32_t kArpLdsSlots = 1024;   // ARP indexes up to 16 KB are staged in LDS
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kShards = 8;             // arrival-ticket shards
@@ -96,7 +97,9 @@ constexpr int kWaitVm0 = 0x0F70;
 // rv4[i]: header + first address word, used for every packet:
 //   x0 = ip_ver | proto << 8 | src_port << 16 and its wildcard mask m0
 //   x1 = dst_port and mask m1; m1 bit 31 (x1 bit 31 clear, so it never decides a match) marks a
-//   rule with IPv6 address words, the only rules an IPv6 key must test against rv6
+//   rule with IPv6 address words, the only rules an IPv6 key must test against rv6; x1 bits
+//   16-17 (m1 bits 16-30 clear) carry the action code (0 drop, 1 forward, 2 any other type),
+//   so the scan hands the matched rule's action over with its index
 //   s0/sm0, d0/dm0: union bytes 0-3 of src/dst as LE u32 (the v4 view, rule_t.src_ip.v4),
 //   pre-masked so a match is ((key ^ x) & m) == 0 for every pair.
 // rv6[i]: union words 1-3 of src/dst (pre-masked) and masks, used only by IPv6 packets.
@@ -212,9 +215,56 @@ struct Args {
     const uint4* tt4;
     const uint4* tt6;
     uint32_t ng4, ng6, tss;
+    // the context's arrays, passed by value so that no kernel waits on a pointer load
+    TilePay* pay;                    // [grid]
+    uint32_t* cand_tile;             // [ntiles]
+    unsigned long long* stats;       // [cap][2]
+    unsigned long long* stats_idx;   // [nrules_pad][2]
+    uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
 };
 
+// ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
+#ifndef UPE_STAMPS
+#define UPE_STAMPS 0
+#endif
+#if UPE_STAMPS
+__device__ unsigned long long g_stamps[8192 * 16];
+#define STAMP(k)                                                                              \
+    do {                                                                                      \
+        if (threadIdx.x == 0) {                                                               \
+            unsigned long long t_;                                                            \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+            g_stamps[blockIdx.x * 16 + (k)] = t_;                                             \
+        }                                                                                     \
+    } while (0)
+#define STAMP_VM(k)                                                                           \
+    do {                                                                                      \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
+        STAMP(k);                                                                             \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#define STAMP_VM(k) do {} while (0)
+#endif
+
 // ---- small helpers ------------------------------------------------------------------------
+// Wave-wide reduction (K = 0 sum, 1 min, 2 max): DPP rotations inside each 16-lane row, then the
+// four row results through scalar registers (no LDS, no shuffle round trips).
+template <int K>
+__device__ __forceinline__ uint32_t dpp_op(uint32_t x, uint32_t y) {
+    return K == 0 ? x + y : K == 1 ? min(x, y) : max(x, y);
+}
+template <int K>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t x) {
+    x = dpp_op<K>(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false));
+    x = dpp_op<K>(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false));
+    x = dpp_op<K>(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false));
+    x = dpp_op<K>(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false));
+    const uint32_t r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
+    return dpp_op<K>(dpp_op<K>(r0, r1), dpp_op<K>(r2, r3));
+}
+
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
 __device__ __forceinline__ uint32_t at2(uint32_t hi, uint32_t lo) {   // dword at byte 4q+2
     return __builtin_amdgcn_alignbit(hi, lo, 16);
@@ -257,6 +307,17 @@ __device__ __forceinline__ bool arp_lookup(const NeighIndex& x, uint32_t ip, uin
     if (x.bits == 0) return false;
     const uint4 e1 = x.t[slot1(ip, x.seed, x.bits)];
     const uint4 e2 = x.t[slot2(ip, x.seed, x.bits)];
+    const bool h1 = ((e1.z >> 16) & 1u) && e1.x == ip;
+    const bool h2 = ((e2.z >> 16) & 1u) && e2.x == ip;
+    lo = h1 ? e1.y : e2.y;
+    hi = (h1 ? e1.z : e2.z) & 0xFFFFu;
+    return h1 || h2;
+}
+// The same lookup against an LDS copy of the slot array.
+__device__ __forceinline__ bool arp_lookup_lds(const uint4* t, uint32_t bits, uint32_t seed,
+                                               uint32_t ip, uint32_t& lo, uint32_t& hi) {
+    const uint4 e1 = t[slot1(ip, seed, bits)];
+    const uint4 e2 = t[slot2(ip, seed, bits)];
     const bool h1 = ((e1.z >> 16) & 1u) && e1.x == ip;
     const bool h2 = ((e2.z >> 16) & 1u) && e2.x == ip;
     lo = h1 ? e1.y : e2.y;
@@ -311,10 +372,14 @@ __device__ __forceinline__ const __attribute__((address_space(4))) V* as_const(c
 // the wave walks the same rules in sorted order; rule words are wave-uniform loads.  `done`
 // lanes (already matched, or not scanning) are ignored.  V6 = some lane holds an IPv6 key; rules
 // without IPv6 address words skip the rv6 test (a scalar branch).
-template <bool V6>
+// Small tables are read from an LDS copy (staged at kernel entry, broadcast reads of a
+// wave-uniform address: no scalar-cache round trip in the dependent chain); larger ones through
+// the scalar unit from the constant address space.
+template <bool V6, bool kLdsRules>
 __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4],
-                                               const uint32_t d[4]) {
+                                               const uint32_t d[4], uint32_t& act,
+                                               const u32x8* l4, const u32x16* l6) {
     uint32_t hit = kNone;
     static_assert(sizeof(RuleV4) == 32 && sizeof(RuleV6) == 64, "rule stream strides");
     const auto* rv4 = as_const<u32x8>(a.rv4);
@@ -325,12 +390,12 @@ __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             // RuleV4 words: x0 m0 x1 m1 s0 sm0 d0 dm0
-            const u32x8 r = rv4[base + u];
+            const u32x8 r = kLdsRules ? l4[base + u] : rv4[base + u];
             uint32_t x = ((k0 ^ r[0]) & r[1]) | ((k1 ^ r[2]) & r[3]) | ((s[0] ^ r[4]) & r[5]) |
                          ((d[0] ^ r[6]) & r[7]);
-            if (V6 && (r[3] & kRuleV6Words)) {
+            if (V6 && (__builtin_amdgcn_readfirstlane(r[3]) & kRuleV6Words)) {
                 // RuleV6 words: s[3] sm[3] d[3] dm[3]
-                const u32x16 q = rv6[base + u];
+                const u32x16 q = kLdsRules ? l6[base + u] : rv6[base + u];
                 const uint32_t y = ((s[1] ^ q[0]) & q[3]) | ((s[2] ^ q[1]) & q[4]) |
                                    ((s[3] ^ q[2]) & q[5]) | ((d[1] ^ q[6]) & q[9]) |
                                    ((d[2] ^ q[7]) & q[10]) | ((d[3] ^ q[8]) & q[11]);
@@ -338,6 +403,7 @@ __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is
             }
             if (!done && x == 0) {
                 hit = base + u;
+                act = r[2];   // the action code rides in x1 bits 16-17 (see RuleV4)
                 done = true;
             }
         }
@@ -367,7 +433,8 @@ __host__ __device__ __forceinline__ uint32_t tss_hash(const uint32_t* k, int nw,
 // of the linear scan (reference src/rule_table.c:163-176).
 template <int F>
 __device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32_t k0, uint32_t k1,
-                                              const uint32_t s[4], const uint32_t d[4]) {
+                                              const uint32_t s[4], const uint32_t d[4],
+                                              uint32_t& act) {
     uint32_t best = kNone;
     const uint32_t ng = F == 4 ? a.ng4 : a.ng6;
     const auto* G = as_const<u32x16>(F == 4 ? a.tg4 : a.tg6);
@@ -401,16 +468,20 @@ __device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32
                 const bool h2 = b2.y && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
                                 a2.w == kw[3];
                 idx = h1 ? b1.x : h2 ? b2.x : kNone;
+                const uint32_t ac = h1 ? b1.z : b2.z;
+                if (idx < best) act = ac << 16;
             } else {
                 const uint4 a1 = T[3 * t1], b1 = T[3 * t1 + 1], c1 = T[3 * t1 + 2];
                 const uint4 a2 = T[3 * t2], b2 = T[3 * t2 + 1], c2 = T[3 * t2 + 2];
-                const bool h1 = c1.w && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
+                const bool h1 = (c1.w & 1u) && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
                                 a1.w == kw[3] && b1.x == kw[4] && b1.y == kw[5] &&
                                 b1.z == kw[6] && b1.w == kw[7] && c1.x == kw[8] && c1.y == kw[9];
-                const bool h2 = c2.w && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
+                const bool h2 = (c2.w & 1u) && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
                                 a2.w == kw[3] && b2.x == kw[4] && b2.y == kw[5] &&
                                 b2.z == kw[6] && b2.w == kw[7] && c2.x == kw[8] && c2.y == kw[9];
                 idx = h1 ? c1.z : h2 ? c2.z : kNone;
+                const uint32_t ac = (h1 ? c1.w : c2.w) >> 8;
+                if (idx < best) act = ac << 16;
             }
             best = min(best, idx);
         }
@@ -607,7 +678,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
     const uint32_t spec = (a.ntiles - 1) % gridDim.x;
     uint32_t pv = 0;
     if (tid < kPayWords)
-        pv = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&S->pay[spec]) + tid,
+        pv = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&a.pay[spec]) + tid,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // small-table rule_stats replicas, kStPer words per thread per round
     constexpr int kStPer = 4;
@@ -644,7 +715,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
     __syncthreads();
 
     // worker totals and this batch's summary
-    if (small && (uint32_t)tid < E && t_st[tid]) atomicAdd(&S->stats_idx[tid], t_st[tid]);
+    if (small && (uint32_t)tid < E && t_st[tid]) atomicAdd(&a.stats_idx[tid], t_st[tid]);
     DevTotals* T = &S->totals;
     if (tid < 8) {
         // upe_counters_t order: pkts_in, then C_PARSED .. C_ARP_REPLY
@@ -672,7 +743,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
         for (uint32_t base = 0; base < tend; base += 64) {
             const uint32_t t = base + (uint32_t)lane;
             // flags were set with device atomics: read and re-arm them the same way
-            const uint32_t cbt = t < tend ? __hip_atomic_exchange(&S->cand_tile[t], 0u,
+            const uint32_t cbt = t < tend ? __hip_atomic_exchange(&a.cand_tile[t], 0u,
                                                                   __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT)
                                           : 0u;
@@ -700,7 +771,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
         }
         // flagged tiles past tend keep their flag: clear them too
         for (uint32_t t = tend + (uint32_t)lane; t < a.ntiles; t += 64)
-            __hip_atomic_store(&S->cand_tile[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.cand_tile[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // New L1 state: the last table hit, if some packet missed the starting entry and hit the
@@ -708,7 +779,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
     // table); otherwise unchanged.
     if (lane == 0 && t_min[M_F4] != kNone && t_max[X_M4] != 0) {
         const uint32_t wg = ((t_max[X_M4] - 1) / kTile) % gridDim.x;
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(&S->pay[wg]);
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(&a.pay[wg]);
         uint32_t v[3];
         for (int j = 0; j < 3; ++j)
             v[j] = wg == spec ? t_pay[j]
@@ -720,7 +791,7 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
     }
     if (lane == 1 && t_min[M_F6] != kNone && t_max[X_M6] != 0) {
         const uint32_t wg = ((t_max[X_M6] - 1) / kTile) % gridDim.x;
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(&S->pay[wg]);
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(&a.pay[wg]);
         uint32_t v[6];
         for (int j = 0; j < 6; ++j)
             v[j] = wg == spec ? t_pay[3 + j]
@@ -745,16 +816,19 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
 template <bool kTssMode>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
-    __shared__ uint32_t s_cnt[C_N];
-    __shared__ uint32_t s_red[kWaves][8];
+    // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6, cand bits
+    __shared__ uint32_t s_wv[kWaves][14];
     __shared__ uint32_t s_pay[kWaves][kPayWords];
-    __shared__ uint32_t s_l1[8];   // starting L1 entries: arp ip, ndp ip[4], look flags
+    __shared__ uint32_t s_lpay[kBlock][kPayWords];   // each lane's latest table hit
+    __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
+    __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_last;    // this workgroup arrived last (set by wave 0)
 #if UPE_GLDS
     __shared__ uint4 s_win[kWaves][256];   // per wave: 64 frames x bytes 0..63 (LDS-DMA target)
 #endif
 
     if (kAblate & 64) return;
+    STAMP(0);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -763,27 +837,45 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
-    if (tid < C_N) s_cnt[tid] = 0;
-    if (tid < 8) {
-        const DevL1* l1 = &a.st->l1;
-        const uint32_t v[8] = {l1->arp_ip, l1->ndp_ip[0], l1->ndp_ip[1], l1->ndp_ip[2],
-                               l1->ndp_ip[3], (l1->arp_ok ? 0u : 1u) | (l1->ndp_ok ? 0u : 2u),
-                               0u, 0u};
-        s_l1[tid] = v[tid];
-    }
-    __syncthreads();
-    const uint32_t look = s_l1[5];   // bit 0: the ARP entry disagrees with the table, bit 1: NDP
-    const bool look4 = look & 1u, look6 = look & 2u;
 
-    // per-wave L1 bookkeeping over this workgroup's tiles (wave-uniform)
-    uint32_t wf4 = kNone, wf6 = kNone, wfc = kNone, wm4 = 0, wm6 = 0, wcb = 0;
-    // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
-    // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
-    // workgroup, at the very end of its life, not once per tile.
-    // descriptors run one tile ahead of the frames they point at
+    // the first descriptor, and small rule tables into LDS, before the entry barrier
     uint64_t dsc_next = 0;
     if (blockIdx.x < a.ntiles && blockIdx.x * kTile + (uint32_t)tid < a.n)
         dsc_next = a.desc[blockIdx.x * kTile + (uint32_t)tid];
+    if (!kTssMode && small_stats) {
+        const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
+        const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
+        uint4* d4 = reinterpret_cast<uint4*>(s_rv4);
+        uint4* d6 = reinterpret_cast<uint4*>(s_rv6);
+        for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) d4[k] = g4[k];
+        for (uint32_t k = tid; k < 4 * a.nrules_pad; k += kBlock) d6[k] = g6[k];
+    }
+    // small ARP indexes (<= 16 KB) into LDS after the rule-stats bins: a lookup is then an LDS
+    // read, not a memory round trip queued behind the batch's frame traffic
+    uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
+    if (a.arp_lds)
+        for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
+    // The starting L1 entries, as wave-uniform (scalar) loads that stay in flight while the
+    // first descriptors and frames load.  DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4],
+    // ndp_mac_lo/hi, arp_ok, ndp_ok.
+    static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
+    const u32x16 l1w = *as_const<u32x16>(&a.st->l1);
+    __syncthreads();
+    const bool look4 = l1w[9] == 0u;    // the ARP entry disagrees with the table
+    const bool look6 = l1w[10] == 0u;   // the NDP entry disagrees with the table
+    STAMP(1);
+
+    // Per-lane accumulators over this workgroup's tiles, reduced once at the end (not per tile):
+    // counters as 16-bit pairs (a lane sees at most one packet per tile, and a workgroup takes
+    // fewer than 2^16 tiles), first / last packet indexes of the L1 bookkeeping as running
+    // min / max; each lane's latest table hit is kept in LDS (tiles ascend, so it is the
+    // lane's last one).
+    uint32_t c01 = 0, c23 = 0, c45 = 0, c67 = 0;
+    uint32_t lf4 = kNone, lf6 = kNone, lfc = kNone, lm4 = 0, lm6 = 0, wcb = 0;
+    // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
+    // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
+    // workgroup, at the very end of its life, not once per tile.
+    // (descriptors run one tile ahead of the frames they point at)
     for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint32_t i = tile * kTile + (uint32_t)tid;
         const bool live = i < a.n;
@@ -849,6 +941,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (nt < a.ntiles && nt * kTile + (uint32_t)tid < a.n) dsc_next = a.desc[nt * kTile + tid];
         }
 
+        if (tile == blockIdx.x) STAMP_VM(2);
         // ---- fast path: option-less IPv4 / IPv6 ----
         const uint32_t e12 = w[3] & 0xFFFFu;          // bytes 12,13 (ethertype, byte-swapped)
         const bool fast4 = live && len >= 34u && e12 == 0x0008u && byte_of(w[3], 2) == 0x45u;
@@ -904,20 +997,40 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const bool ctrl = live && (r.consumed || (r.flags & UPE_VF_ARP_LEARN));
         const bool ok = live && r.ok && !r.consumed;
 
+        // ---- next hop, looked up before the rule scan: it needs only the destination, so its
+        // latency hides behind the scan (the answer is unused unless the packet is forwarded) ----
+        uint32_t mlo = 0, mhi = 0;
+        bool nhit = false;
+        if (ok && r.ttl > 1u && !(kAblate & 2)) {
+            if (!r.v6)
+                nhit = a.arp_lds ? arp_lookup_lds(s_arp, a.arp.bits, a.arp.seed, r.d[0], mlo, mhi)
+                                 : arp_lookup(a.arp, r.d[0], mlo, mhi);
+            else
+                nhit = ndp_lookup(a.ndp, r.d, mlo, mhi);
+        }
+
         // ---- rule_table_match ----
         const uint32_t k0 = (r.v6 ? 6u : 4u) | (r.proto << 8) | (r.sport << 16);
         const uint32_t k1 = r.dport;
         const bool need_v6 = __any(ok && r.v6);
-        uint32_t ri;
+        uint32_t ri, act = 0;   // act: the matched rule's x1 word (action code in bits 16-17)
         if (kAblate & 1) {
             ri = ok ? 0u : kNone;
+            act = 1u << 16;
         } else if (kTssMode) {
-            const uint32_t r4 = tss_match<4>(a, ok && !r.v6, k0, k1, r.s, r.d);
-            const uint32_t r6 = need_v6 ? tss_match<6>(a, ok && r.v6, k0, k1, r.s, r.d) : kNone;
+            uint32_t a4 = 0, a6 = 0;
+            const uint32_t r4 = tss_match<4>(a, ok && !r.v6, k0, k1, r.s, r.d, a4);
+            const uint32_t r6 =
+                need_v6 ? tss_match<6>(a, ok && r.v6, k0, k1, r.s, r.d, a6) : kNone;
             ri = r.v6 ? r6 : r4;
+            act = r.v6 ? a6 : a4;
         } else {
-            ri = need_v6 ? scan_rules<true>(a, !ok, r.v6, k0, k1, r.s, r.d)
-                         : scan_rules<false>(a, !ok, r.v6, k0, k1, r.s, r.d);
+            if (small_stats)
+                ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
+                             : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6);
+            else
+                ri = need_v6 ? scan_rules<true, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
+                             : scan_rules<false, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6);
         }
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
@@ -929,39 +1042,37 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else if (ri == kNone) {
             code = UPE_V_DROP_NOMATCH;
         } else {
-            const int2 info = a.rinfo[ri];
+            const uint32_t ac = (act >> 16) & 3u;
             rbits = (ri + 1) << 8;
             // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: an LDS histogram below for
             // LDS-resident tables; for larger ones upe_rule_hist folds the verdict words after
             // the launch (one scattered device atomic per packet would cost more than the
             // whole classification)
-            code = info.x == UPE_ACT_DROP ? UPE_V_DROP_RULE
-                 : info.x == UPE_ACT_FWD  ? UPE_V_FWD
-                                          : UPE_V_DROP_ACTION;
+            code = ac == 0u ? UPE_V_DROP_RULE : ac == 1u ? UPE_V_FWD : UPE_V_DROP_ACTION;
         }
         uint32_t flags = r.flags;
+        if (tile == blockIdx.x) STAMP_VM(3);
 
         // ---- L3 forward (src/worker.c:155-244) ----
         bool fp4 = false, fp6 = false;       // this packet misses the start entry, hits table
         bool thit4 = false, thit6 = false;   // the table answered this packet
         bool hit = false;      // the packet gets a MAC: the table's (or the starting entry's)
         bool cand = false;     // destination == starting L1 entry (ARP: and != 0)
-        uint32_t mlo = 0, mhi = 0;
         bool wrote1 = false;
         if (code == UPE_V_FWD) {
             if (r.ttl <= 1u) {                         // src/worker.c:165-172, 204-211
                 code = UPE_V_DROP_TTL;
             } else if (!r.v6) {
                 wrote1 = true;
-                hit = !(kAblate & 2) && arp_lookup(a.arp, r.d[0], mlo, mhi);
-                cand = s_l1[0] != 0 && r.d[0] == s_l1[0];
+                hit = nhit;
+                cand = l1w[0] != 0 && r.d[0] == l1w[0];
                 fp4 = !cand && hit;
                 thit4 = hit;
             } else {
                 wrote1 = true;
-                hit = !(kAblate & 2) && ndp_lookup(a.ndp, r.d, mlo, mhi);
-                cand = r.d[0] == s_l1[1] && r.d[1] == s_l1[2] && r.d[2] == s_l1[3] &&
-                       r.d[3] == s_l1[4];
+                hit = nhit;
+                cand = r.d[0] == l1w[3] && r.d[1] == l1w[4] && r.d[2] == l1w[5] &&
+                       r.d[3] == l1w[6];
                 fp6 = !cand && hit;
                 thit6 = hit;
             }
@@ -986,58 +1097,75 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             atomicAdd(&lds_hist[2 * ri + 1], len);
         }
 
-        // ---- per-wave totals and L1 bookkeeping ----
-        const uint32_t wc[C_N] = {
-            (uint32_t)__popcll(__ballot(ok)),
-            (uint32_t)__popcll(__ballot(ok && ri != kNone)),
-            (uint32_t)__popcll(__ballot(live && code == UPE_V_FWD)),
-            (uint32_t)__popcll(__ballot(live && code != UPE_V_FWD && code != UPE_V_CONSUMED)),
-            (uint32_t)__popcll(__ballot(live && r.consumed)),
-            (uint32_t)__popcll(__ballot(live && !r.consumed && (r.flags & UPE_VF_ARP_LEARN))),
-            (uint32_t)__popcll(__ballot(live && !r.consumed && (r.flags & UPE_VF_ARP_REPLY))),
-            (uint32_t)__popcll(__ballot(ctrl)), 0u};
+        // ---- per-lane totals and L1 bookkeeping ----
+        c01 += (ok ? 1u : 0u) + (ok && ri != kNone ? 0x10000u : 0u);
+        c23 += (live && code == UPE_V_FWD ? 1u : 0u) +
+               (live && code != UPE_V_FWD && code != UPE_V_CONSUMED ? 0x10000u : 0u);
+        c45 += (live && r.consumed ? 1u : 0u) +
+               (live && !r.consumed && (r.flags & UPE_VF_ARP_LEARN) ? 0x10000u : 0u);
+        c67 += (live && !r.consumed && (r.flags & UPE_VF_ARP_REPLY) ? 1u : 0u) +
+               (ctrl ? 0x10000u : 0u);
+        lf4 = min(lf4, fp4 ? i : kNone);
+        lf6 = min(lf6, fp6 ? i : kNone);
+        lfc = min(lfc, ctrl ? i : kNone);
+        lm4 = max(lm4, thit4 ? i + 1 : 0u);
+        lm6 = max(lm6, thit6 ? i + 1 : 0u);
+        if (thit4) {
+            s_lpay[tid][0] = r.d[0]; s_lpay[tid][1] = mlo; s_lpay[tid][2] = mhi;
+        }
+        if (thit6) {
+            s_lpay[tid][3] = r.d[0]; s_lpay[tid][4] = r.d[1]; s_lpay[tid][5] = r.d[2];
+            s_lpay[tid][6] = r.d[3]; s_lpay[tid][7] = mlo; s_lpay[tid][8] = mhi;
+        }
+        if (look4 || look6) {
+            // packets the starting entry answers if nothing before them missed it and hit the
+            // table: flag the tile, and drain this wave's stores so the release below covers them
+            const uint32_t cbits = (__ballot(cand && !r.v6 && look4) ? 1u : 0u) |
+                                   (__ballot(cand && r.v6 && look6) ? 2u : 0u);
+            if (cbits) {
+                if (lane == 0) atomicOr(&a.cand_tile[tile], cbits);
+                wcb = __builtin_amdgcn_readfirstlane(wcb | cbits);
+                __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            }
+        }
+    }
+    STAMP(4);
+    // ---- reduce the per-lane accumulators: DPP rotations inside each 16-lane row, then the four
+    // row results through scalar registers; then across the workgroup's waves in LDS ----
+    {
+        const uint32_t cs[8] = {c01 & 0xFFFFu, c01 >> 16, c23 & 0xFFFFu, c23 >> 16,
+                                c45 & 0xFFFFu, c45 >> 16, c67 & 0xFFFFu, c67 >> 16};
+        const int w = wave;
+        if (lane == 0) {
 #pragma unroll
-        for (int c = 0; c < C_N; ++c)
-            if (lane == 0 && wc[c]) atomicAdd(&s_cnt[c], wc[c]);
-        // lane order is packet order, so first / last qualifying packets are ballot bit scans
-        const uint32_t i0 = tile * kTile + (uint32_t)wave * 64u;
-        const unsigned long long bf4 = __ballot(fp4), bf6 = __ballot(fp6), bfc = __ballot(ctrl);
-        const unsigned long long bm4 = __ballot(thit4), bm6 = __ballot(thit6);
-        const uint32_t f4 = bf4 ? i0 + (uint32_t)__ffsll((long long)bf4) - 1 : kNone;
-        const uint32_t f6 = bf6 ? i0 + (uint32_t)__ffsll((long long)bf6) - 1 : kNone;
-        const uint32_t fc = bfc ? i0 + (uint32_t)__ffsll((long long)bfc) - 1 : kNone;
-        const uint32_t m4 = bm4 ? i0 + 64u - (uint32_t)__clzll((long long)bm4) : 0u;   // index + 1
-        const uint32_t m6 = bm6 ? i0 + 64u - (uint32_t)__clzll((long long)bm6) : 0u;
-        // packets the starting entry answers if nothing before them missed it and hit the table
-        const uint32_t cbits = (__ballot(cand && !r.v6 && look4) ? 1u : 0u) |
-                               (__ballot(cand && r.v6 && look6) ? 2u : 0u);
-        // later tiles hold later packets: a hit here supersedes the wave's earlier payload
-        if (m4 && i + 1 == m4) {
-            s_pay[wave][0] = r.d[0]; s_pay[wave][1] = mlo; s_pay[wave][2] = mhi;
+            for (int c = 0; c < 8; ++c) s_wv[w][c] = 0;
         }
-        if (m6 && i + 1 == m6) {
-            s_pay[wave][3] = r.d[0]; s_pay[wave][4] = r.d[1]; s_pay[wave][5] = r.d[2];
-            s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
+        uint32_t v[13];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = wave_reduce<0>(cs[c]);
+        v[8] = wave_reduce<1>(lf4);
+        v[9] = wave_reduce<1>(lf6);
+        v[10] = wave_reduce<1>(lfc);
+        v[11] = wave_reduce<2>(lm4);
+        v[12] = wave_reduce<2>(lm6);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 13; ++c) s_wv[w][c] = v[c];
+            s_wv[w][13] = wcb;
         }
-        // wave-uniform: keep the running values in SGPRs
-        wf4 = __builtin_amdgcn_readfirstlane(min(wf4, f4));
-        wf6 = __builtin_amdgcn_readfirstlane(min(wf6, f6));
-        wfc = __builtin_amdgcn_readfirstlane(min(wfc, fc));
-        wm4 = __builtin_amdgcn_readfirstlane(max(wm4, m4));
-        wm6 = __builtin_amdgcn_readfirstlane(max(wm6, m6));
-        if (cbits) {
-            // packets the last workgroup may rewrite: flag the tile, and drain this wave's
-            // stores so the release below covers them
-            if (lane == 0) atomicOr(&a.st->cand_tile[tile], cbits);
-            wcb = __builtin_amdgcn_readfirstlane(wcb | cbits);
-            __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        }
+        // the lane holding the wave's last table hit per family hands over its payload
+        if (v[11] && lm4 == v[11])
+            for (int j = 0; j < 3; ++j) s_pay[w][j] = s_lpay[tid][j];
+        if (v[12] && lm6 == v[12])
+            for (int j = 3; j < kPayWords; ++j) s_pay[w][j] = s_lpay[tid][j];
     }
-    if (lane == 0) {
-        s_red[wave][0] = wf4; s_red[wave][1] = wf6; s_red[wave][2] = wm4;
-        s_red[wave][3] = wm6; s_red[wave][4] = wfc; s_red[wave][5] = wcb;
-    }
-    __syncthreads();
+    STAMP(9);
+    // A bare barrier: LDS drained (lgkmcnt), global stores left in flight.  Nothing after this
+    // point reads the frames or verdicts this workgroup wrote, except the last workgroup's
+    // repair pass, and waves holding such packets drained and flagged their stores in the loop;
+    // __syncthreads() would make every wave wait for its write acknowledgements.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    STAMP(10);
 
     // ---- rule_stats of mid-size tables: straight into the worker totals (the host reads them
     // after the batch; nothing in this launch does) ----
@@ -1045,7 +1173,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) {
             const uint32_t v = lds_hist[k];
             if (v)
-                atomicAdd(&a.st->stats[2 * (uint32_t)a.rinfo[k >> 1].y + (k & 1)],
+                atomicAdd(&a.stats[2 * (uint32_t)a.rinfo[k >> 1].y + (k & 1)],
                           (unsigned long long)v);
         }
     }
@@ -1059,21 +1187,24 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     int w4 = 0, w6 = 0;
 #pragma unroll
     for (int v = 0; v < kWaves; ++v) {
-        cb |= s_red[v][5];
-        if (s_red[v][2] > x4) { x4 = s_red[v][2]; w4 = v; }
-        if (s_red[v][3] > x6) { x6 = s_red[v][3]; w6 = v; }
+        cb |= s_wv[v][13];
+        if (s_wv[v][11] > x4) { x4 = s_wv[v][11]; w4 = v; }
+        if (s_wv[v][12] > x6) { x6 = s_wv[v][12]; w6 = v; }
     }
     const bool flag = (look4 || look6) && cb;
     if (!(kAblate & 4)) {
         if (lane < C_N) {
-            const uint32_t cv = lane == C_CAND ? (flag ? 1u : 0u) : s_cnt[lane];
+            uint32_t cv = 0;
+#pragma unroll
+            for (int v = 0; v < kWaves; ++v) cv += lane < 8 ? s_wv[v][lane] : 0u;
+            if (lane == C_CAND) cv = flag ? 1u : 0u;
             if (cv) atomicAdd(&S->acc.cnt[rep][lane], cv);
         }
         if (lane < M_N) {
-            const int src = lane == M_F4 ? 0 : lane == M_F6 ? 1 : 4;
+            // M_F4, M_F6, M_CTRL <- wave slots 8, 9, 10
             uint32_t mv = kNone;
 #pragma unroll
-            for (int v = 0; v < kWaves; ++v) mv = min(mv, s_red[v][src]);
+            for (int v = 0; v < kWaves; ++v) mv = min(mv, s_wv[v][8 + lane]);
             if (mv != kNone) atomicMin(&S->acc.mins[rep][lane], mv);
         }
         if (lane < X_N) {
@@ -1089,7 +1220,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     }
     // the workgroup's last table hit per family (only the one holding the batch maximum is read)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(&S->pay[blockIdx.x]) + lane,
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(&a.pay[blockIdx.x]) + lane,
                            s_pay[lane < 3 ? w4 : w6][lane], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (flag) {
@@ -1097,8 +1228,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // to the last workgroup (release: write back this XCD's L2)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
+    STAMP(5);
     // every atomic and payload store of this workgroup is performed before the arrival ticket
     __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    STAMP(6);
     uint32_t last = 0;
     if (lane == 0) {
         const uint32_t nb = gridDim.x;
@@ -1111,11 +1244,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                           __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
     }
     if (lane == 0) s_last = last;
+    STAMP(7);
     }   // wave 0
     // the other waves wait here, so the last workgroup folds the batch with all its threads
     __syncthreads();
     if (!s_last) return;
     batch_tail(a, tid, look4, look6);
+    STAMP(8);
 }
 
 
@@ -1188,6 +1323,7 @@ int fail(const std::string& msg) {
             return fail(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
     } while (0)
 
+uint32_t act_code(int32_t type) { return type == UPE_ACT_DROP ? 0u : type == UPE_ACT_FWD ? 1u : 2u; }
 uint32_t mac_lo(const uint8_t* m) {
     return (uint32_t)m[0] | ((uint32_t)m[1] << 8) | ((uint32_t)m[2] << 16) | ((uint32_t)m[3] << 24);
 }
@@ -1585,13 +1721,14 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
             if (slot[t] < 0) continue;
             const Key& k = keys[slot[t]];
             uint4* e = &out.slots[base + t * per];
+            const uint32_t act = act_code(rules[idx[slot[t]]].action.type);
             if (F == 4) {
                 e[0] = make_uint4(k[0], k[1], k[2], k[3]);
-                e[1] = make_uint4(idx[slot[t]], 1u, 0u, 0u);
+                e[1] = make_uint4(idx[slot[t]], 1u, act, 0u);
             } else {
                 e[0] = make_uint4(k[0], k[1], k[2], k[3]);
                 e[1] = make_uint4(k[4], k[5], k[6], k[7]);
-                e[2] = make_uint4(k[8], k[9], idx[slot[t]], 1u);
+                e[2] = make_uint4(k[8], k[9], idx[slot[t]], 1u | (act << 8));
             }
         }
     }
@@ -1641,7 +1778,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         a.x0 = (uint32_t)r.ip_ver | ((uint32_t)r.protocol << 8) | ((uint32_t)r.src_port << 16);
         a.m0 = (r.ip_ver ? 0xFFu : 0u) | (r.protocol ? 0xFF00u : 0u) |
                (r.src_port ? 0xFFFF0000u : 0u);
-        a.x1 = r.dst_port;
+        a.x1 = (uint32_t)r.dst_port | (act_code(r.action.type) << 16);
         a.m1 = r.dst_port ? 0xFFFFu : 0u;
         const uint8_t* si = r.src_ip.v6;
         const uint8_t* sm = r.src_mask.v6;
@@ -1894,8 +2031,17 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
     a.tss = c->tss ? 1u : 0u;
+    a.pay = c->pay;
+    a.cand_tile = c->cand_tile;
+    a.stats = c->stats;
+    a.stats_idx = c->stats_idx;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
-    const size_t lds = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
+    const size_t hist = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
+    // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
+    // array 16-byte aligned after the bins)
+    const uint32_t arp_slots = c->arp_bits ? (1u << c->arp_bits) : 0u;
+    a.arp_lds = (arp_slots && arp_slots <= kArpLdsSlots && hist <= 8192) ? arp_slots : 0u;
+    const size_t lds = hist + (size_t)a.arp_lds * sizeof(uint4);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     if (c->resident_lds != lds || c->resident == 0 || c->resident_tss != c->tss) {
         c->resident_tss = c->tss;
@@ -2028,6 +2174,22 @@ int upe_gpu_host_free(void* p) {
     if (p) HIP_TRY(hipHostFree(p));
     return 0;
 }
+
+int upe_gpu_process_batches(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list, const uint64_t* d_desc,
+                            uint32_t* d_verdict, size_t n, size_t count, void* stream) {
+    if (!c) return fail("null context");
+    if (count && !d_frames_list) return fail("null frames list");
+    for (size_t k = 0; k < count; ++k)
+        if (upe_gpu_process(c, d_frames_list[k], d_desc, d_verdict, n, stream) != 0) return -1;
+    return 0;
+}
+
+#if UPE_STAMPS
+int upe_gpu_diag_stamps(void* host, size_t bytes) {
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
+    return 0;
+}
+#endif
 
 int upe_gpu_sync(upe_gpu_ctx_t* c, void* stream) {
     if (!c) return fail("null context");

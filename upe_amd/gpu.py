@@ -56,6 +56,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_memcpy_h2d": (I, [P, P, P, SZ, P]),
         "upe_gpu_memcpy_d2h": (I, [P, P, P, SZ, P]),
         "upe_gpu_process_host": (I, [P, P, SZ, P, P, SZ, SZ]),
+        "upe_gpu_process_batches": (I, [P, P, P, P, SZ, SZ, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
     }
@@ -75,6 +76,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
+            "upe_gpu_process_batches",
             "upe_gpu_host_alloc", "upe_gpu_host_free")
 
 
@@ -174,6 +176,13 @@ class GpuWorker:
         _check(LIB.upe_gpu_process(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
                                    _dev_ptr(verdict), n, stream or None),
                "upe_gpu_process")
+
+    def process_batches(self, frames_ptrs, desc, verdict, n: int, stream=None) -> None:
+        """Queue len(frames_ptrs) batches (device pointers) back to back from native code."""
+        arr = (ctypes.c_void_p * len(frames_ptrs))(*[int(x) for x in frames_ptrs])
+        _check(LIB.upe_gpu_process_batches(self._ctx, arr, _dev_ptr(desc), _dev_ptr(verdict), n,
+                                           len(frames_ptrs), stream or None),
+               "upe_gpu_process_batches")
 
     def sync(self, stream=None) -> None:
         _check(LIB.upe_gpu_sync(self._ctx, stream or None), "upe_gpu_sync")
