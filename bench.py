@@ -97,7 +97,7 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
     """Host-inclusive rate: the batch starts and ends in pinned host memory (libpcap in, AF_PACKET
     out): upe_gpu_process_host pipelines H2D of frames + descriptors, classify and D2H of verdicts
     + rewritten header bytes over chunks.  windows: ship 96-byte header windows, not frames."""
-    from upe_amd import gpu, synth
+    from upe_amd import gpu, shard, synth
     from upe_amd.layout import FRAME_TAIL, REWRITE_EXTENT, desc_lens, desc_offsets
 
     src = synth.header_windows(wl) if windows else wl
@@ -222,20 +222,11 @@ def main() -> None:
         hr = host_roundtrip(worker, wl, args.host_reps, args.host_chunk,
                             windows=args.config != "B")
 
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([n * args.steps], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        total_packets = float(tot.item())
-        if hr:
-            ht = torch.tensor([hr["seconds"]], dtype=torch.float64, device=dev)
-            dist.all_reduce(ht, op=dist.ReduceOp.MAX)
-            hr["seconds"] = float(ht.item())
-    else:
-        total_packets = float(n * args.steps)
+    # the job ends when the slowest shard does; value = every rank's packets / that time
+    elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
+    total_packets = float(shard.sum_over_ranks([n * args.steps], dist, dev)[0])
+    if hr:
+        hr["seconds"] = shard.max_over_ranks(hr["seconds"], dist, dev)
 
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first)
