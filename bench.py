@@ -65,6 +65,16 @@ def algorithmic_bytes(wl, verdict: np.ndarray) -> np.ndarray:
     return 8 + E + 4 + W
 
 
+def pmc_traffic(config: str, packets: int):
+    """HBM bytes per classify launch from the committed PMC passes of this kernel
+    (profiles/pmc_config<X>.json, made by tools/pmc_run.sh + tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return d["traffic_bytes_per_launch"] if d.get("packets") == packets else None
+
+
 def cpu_baseline(wl, threads: int) -> dict:
     import oracle
 
@@ -230,6 +240,7 @@ def main() -> None:
 
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first)
+        traffic = pmc_traffic(args.config, n)
         bytes_per_launch = float(bpp.sum())
         kern_s = classify_ms / launches / 1e3 if launches else float("nan")
         achieved = bytes_per_launch / kern_s / 1e9
@@ -256,7 +267,9 @@ def main() -> None:
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": (f"profiles/pmc_config{args.config}.json (rocprofv3 PMC, "
+                                   "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
                 "kernel": "upe_classify",
                 "kernel_ms": round(kern_s * 1e3, 5),
                 "finalize_ms": round(finalize_ms / max(launches, 1), 5),

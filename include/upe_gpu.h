@@ -275,6 +275,34 @@ int upe_gpu_free(upe_gpu_ctx_t *ctx, void *dptr);
 int upe_gpu_memcpy_h2d(upe_gpu_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int upe_gpu_memcpy_d2h(upe_gpu_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Host-side batch builders (upe_amd/csrc/upe_host.c, C)                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Load a rule file in the reference's INI format (reference src/rule_config.c:129-282,
+ * rules.example) into rules[0..capacity) as rule_table_init(capacity) + rule_config_load would
+ * leave rt->rules: rule_id = insertion index, wildcard addresses zeroed, sorted by
+ * (priority, rule_id) (src/rule_table.c:130-161).  *count = rules loaded.  0 / -1 (the message,
+ * with the reference's "rules:<line>: ..." wording, in upe_host_last_error()). */
+int upe_rules_load_ini(const char *path, upe_rule_t *rules, size_t capacity, size_t *count);
+
+/* A pcap capture (LE/BE, usec/nsec, link type Ethernet) -> the packed batch layout above, in
+ * record order, as reference src/rx_pcap.c:42-93 admits packets: records with caplen > 2048
+ * (PKTBUF_DATA_SIZE) are dropped.  Call with frames = desc = NULL to size the buffers
+ * (info->packets descriptors, info->frames_bytes bytes including the UPE_FRAME_TAIL), then again
+ * to fill them.  0 / -1. */
+typedef struct {
+    uint64_t records;          /* records in the file */
+    uint64_t packets;          /* packets in the batch */
+    uint64_t dropped_oversize; /* caplen > 2048: dropped by RX, never reach the worker */
+    uint64_t frames_bytes;     /* frames buffer size needed */
+} upe_pcap_info_t;
+int upe_pcap_read(const char *path, uint8_t *frames, size_t frames_cap, uint64_t *desc,
+                  size_t desc_cap, upe_pcap_info_t *info);
+
+/* Last error of the host-side builders on this thread ("" if none). */
+const char *upe_host_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -229,6 +229,20 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
     return rc;
 }
 
+/* ---- the reference's rule-file loader (src/rule_config.c:129-282) into a fresh table -------- */
+#include "rule_config.h"
+
+int upe_refh_rules_load(const char *path, size_t capacity, upe_rule_t *out, size_t *count) {
+    rule_table_t rt;
+    if (rule_table_init(&rt, capacity) != 0) return -2;
+    log_set_level(LOG_ERROR); /* only the reference's error lines */
+    int rc = rule_config_load(path, &rt);
+    memcpy(out, rt.rules, rt.count * sizeof(rule_t));
+    *count = rt.count;
+    rule_table_destroy(&rt);
+    return rc;
+}
+
 /* ---- timed CPU baseline ------------------------------------------------------------------- */
 
 typedef struct {

@@ -60,6 +60,11 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
     }
+    sig.update({
+        "upe_rules_load_ini": (I, [ctypes.c_char_p, P, SZ, P]),
+        "upe_pcap_read": (I, [ctypes.c_char_p, P, SZ, P, SZ, P]),
+        "upe_host_last_error": (ctypes.c_char_p, []),
+    })
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -76,7 +81,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
-            "upe_gpu_process_batches",
+            "upe_gpu_process_batches", "upe_rules_load_ini", "upe_pcap_read",
+            "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free")
 
 
@@ -243,6 +249,35 @@ class GpuWorker:
     def d2h(self, host: np.ndarray, dptr: int, stream=None) -> None:
         _check(LIB.upe_gpu_memcpy_d2h(self._ctx, _np_ptr(host), dptr, host.nbytes, stream or None),
                "upe_gpu_memcpy_d2h")
+
+
+# ---- host-side batch builders (upe_host.c; no GPU needed) ----------------------------------
+
+PCAP_INFO_DTYPE = np.dtype([("records", "<u8"), ("packets", "<u8"), ("dropped_oversize", "<u8"),
+                            ("frames_bytes", "<u8")])
+
+
+def rules_load_ini(path: str, capacity: int = 1024) -> np.ndarray:
+    """upe_rules_load_ini: rt->rules after rule_table_init(capacity) + rule_config_load."""
+    out = np.zeros(capacity, RULE_DTYPE)
+    count = np.zeros(1, np.uint64)
+    rc = LIB.upe_rules_load_ini(os.fsencode(path), _np_ptr(out), capacity, _np_ptr(count))
+    if rc != 0:
+        raise UpeGpuError(LIB.upe_host_last_error().decode())
+    return out[: int(count[0])].copy()
+
+
+def pcap_read(path: str):
+    """upe_pcap_read: a pcap capture -> (frames, desc, info) in the batch layout."""
+    info = np.zeros(1, PCAP_INFO_DTYPE)
+    if LIB.upe_pcap_read(os.fsencode(path), None, 0, None, 0, _np_ptr(info)) != 0:
+        raise UpeGpuError(LIB.upe_host_last_error().decode())
+    frames = np.zeros(int(info["frames_bytes"][0]) + 128, np.uint8)
+    desc = np.zeros(max(int(info["packets"][0]), 1), np.uint64)
+    if LIB.upe_pcap_read(os.fsencode(path), _np_ptr(frames), frames.nbytes, _np_ptr(desc),
+                         desc.shape[0], _np_ptr(info)) != 0:
+        raise UpeGpuError(LIB.upe_host_last_error().decode())
+    return frames, desc[: int(info["packets"][0])].copy(), info
 
 
 class PinnedArray:
