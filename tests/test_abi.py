@@ -21,7 +21,7 @@ HEADER = os.path.join(ROOT, "include", "upe_gpu.h")
 def declared_symbols():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(upe_gpu_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(upe_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_loads_and_exports_every_declared_symbol():
