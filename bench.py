@@ -107,7 +107,7 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
     """Host-inclusive rate: the batch starts and ends in pinned host memory (libpcap in, AF_PACKET
     out): upe_gpu_process_host pipelines H2D of frames + descriptors, classify and D2H of verdicts
     + rewritten header bytes over chunks.  windows: ship 96-byte header windows, not frames."""
-    from upe_amd import gpu, shard, synth
+    from upe_amd import gpu, synth
     from upe_amd.layout import FRAME_TAIL, REWRITE_EXTENT, desc_lens, desc_offsets
 
     src = synth.header_windows(wl) if windows else wl
@@ -169,7 +169,7 @@ def main() -> None:
     else:
         torch.cuda.set_device(local)
 
-    from upe_amd import gpu, synth
+    from upe_amd import gpu, shard, synth
 
     # this rank's static shard: a full batch of the configuration, its own seed
     make = {"B": synth.config_b, "C": synth.config_c, "D": synth.config_d}[args.config]
