@@ -150,8 +150,10 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-copies", type=int, default=1024)
-    ap.add_argument("--host-reps", type=int, default=10,
-                    help="passes of the host round-trip leg (0: skip it)")
+    ap.add_argument("--host-reps", type=int, default=0,
+                    help="passes of the host round-trip leg (default 0: skip it, so that a "
+                         "rocprof summary of the default command holds only full-batch "
+                         "launches; DESIGN.md quotes a --host-reps 10 run)")
     ap.add_argument("--host-chunk", type=int, default=0)
     args = ap.parse_args()
 

@@ -15,9 +15,12 @@ packets = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 vals = {}
 for name in ("fetch", "write"):
     f = glob.glob(f"gpurun_out/pmc_{cfg}/{name}/p_counter_collection.csv")[0]
+    rows = [r for r in csv.DictReader(open(f)) if "upe_classify" in r["Kernel_Name"]]
+    # only the full-batch launches (the bench's host leg launches smaller chunks)
+    gmax = max(int(r["Grid_Size"]) for r in rows)
     acc = collections.defaultdict(float)
-    for r in csv.DictReader(open(f)):
-        if "upe_classify" in r["Kernel_Name"]:
+    for r in rows:
+        if int(r["Grid_Size"]) == gmax:
             acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
     v = sorted(acc.values())
     vals[name] = v[len(v) // 2]           # median dispatch
