@@ -249,6 +249,20 @@ int upe_gpu_process_batches(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
                             const uint64_t *d_desc, uint32_t *d_verdict, size_t n, size_t count,
                             void *stream);
 
+/* upe_gpu_process() plus software RSS in the same pass (reference src/rx_pcap.c:67-77 parses
+ * every packet a second time on the RX thread for this): d_flow_hash[i] (device, n uint32) =
+ * flow_hash() of the packet's flow key (src/parser.c:113-135) when parse_flow_key succeeds, 0
+ * otherwise (verdict code DROP_PARSE or CONSUMED says which).  A caller spreading a capture over
+ * workers takes hash & (workers - 1), as the reference's RX thread does. */
+int upe_gpu_process_rss(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                        uint32_t *d_verdict, uint32_t *d_flow_hash, size_t n, void *stream);
+
+/* Egress list: d_index[0..*d_count) = the indexes i < n whose verdict code is `code` (e.g.
+ * UPE_V_FWD), in packet order — the order process_packet queues frames for tx_send_batch
+ * (reference src/worker.c:240-243, 287-303).  Device buffers; d_index holds n entries. */
+int upe_gpu_compact(upe_gpu_ctx_t *ctx, const uint32_t *d_verdict, size_t n, uint32_t code,
+                    uint32_t *d_index, uint64_t *d_count, void *stream);
+
 /* Wait for all work queued on the context's stream (or `stream`). */
 int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
 

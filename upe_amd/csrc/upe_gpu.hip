@@ -221,6 +221,7 @@ struct Args {
     unsigned long long* stats;       // [cap][2]
     unsigned long long* stats_idx;   // [nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
+    uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
 };
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
@@ -1089,6 +1090,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
         if (live) a.verdict[i] = code | flags | rbits;
+        if (a.flow_hash && live) {
+            // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
+            // key parse_flow_key gives the RX thread (src/rx_pcap.c:71-72), 0 if it fails
+            uint32_t h = r.sport ^ r.dport ^ r.proto;
+            h ^= r.v6 ? (r.s[0] ^ r.s[1] ^ r.s[2] ^ r.s[3] ^ r.d[0] ^ r.d[1] ^ r.d[2] ^ r.d[3])
+                      : (r.s[0] ^ r.d[0]);
+            a.flow_hash[i] = ok ? h : 0u;
+        }
 
         // ---- rule_stats: LDS histogram (same-address lanes serialise in the LDS atomic unit,
         // cheaper than a cross-lane reduction per distinct rule) ----
@@ -1307,6 +1316,64 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
 }
 
 // ------------------------------------------------------------------------------------------
+// Egress list: the indexes of the packets with a given verdict code, in packet order (the order
+// process_packet queues frames for tx_send_batch, reference src/worker.c:240-243).  Pass 1
+// counts per block; pass 2 gives each block its offset (sum of the counts before it) and writes
+// its indexes with wave ballots.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kCompactBlock = 4096;   // packets per workgroup (256 threads x 16)
+
+__global__ void __launch_bounds__(256) upe_compact_count(const uint32_t* verdict, uint32_t n,
+                                                         uint32_t code, uint32_t* counts) {
+    __shared__ uint32_t s_c;
+    if (threadIdx.x == 0) s_c = 0;
+    __syncthreads();
+    const uint32_t p0 = blockIdx.x * kCompactBlock;
+    uint32_t c = 0;
+    for (uint32_t k = threadIdx.x; k < kCompactBlock; k += 256) {
+        const uint32_t i = p0 + k;
+        c += (i < n && (verdict[i] & 0xFu) == code) ? 1u : 0u;
+    }
+    c = wave_reduce<0>(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_c, c);
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = s_c;
+}
+
+__global__ void __launch_bounds__(256) upe_compact_write(const uint32_t* verdict, uint32_t n,
+                                                         uint32_t code, const uint32_t* counts,
+                                                         uint32_t nblocks, uint32_t* index,
+                                                         unsigned long long* total) {
+    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_wave[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t pre = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 256) pre += counts[b];
+    pre = wave_reduce<0>(pre);
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    if (lane == 0 && pre) atomicAdd(&s_base, pre);
+    __syncthreads();
+    uint32_t base = s_base;
+    const uint32_t p0 = blockIdx.x * kCompactBlock;
+    for (uint32_t k = 0; k < kCompactBlock; k += 256) {
+        const uint32_t i = p0 + k + threadIdx.x;
+        const bool m = i < n && (verdict[i] & 0xFu) == code;
+        const unsigned long long bal = __ballot(m);
+        if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t off = base;
+        for (int v = 0; v < wave; ++v) off += s_wave[v];
+        const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (m) index[off + rank] = i;
+        const uint32_t tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        __syncthreads();
+        base += tot;
+    }
+    if (blockIdx.x == nblocks - 1 && threadIdx.x == 0) *total = base;
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 thread_local std::string g_err;
@@ -1351,6 +1418,8 @@ struct upe_gpu_ctx {
     uint4* tt6 = nullptr;
     uint32_t ng4 = 0, ng6 = 0;
     bool tss = false;
+    uint32_t* compact_counts = nullptr;   // upe_gpu_compact: per-block counts
+    size_t compact_alloc = 0;
     // neighbour tables (reachable-entry indexes)
     uint4* arp = nullptr;
     uint32_t arp_bits = 0, arp_seed = 0;
@@ -1590,7 +1659,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6};
+                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->compact_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1980,6 +2049,11 @@ int upe_gpu_get_l1(upe_gpu_ctx_t* c, upe_l1_state_t* l1) {
 
 int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
                     uint32_t* d_verdict, size_t n, void* stream) {
+    return upe_gpu_process_rss(c, d_frames, d_desc, d_verdict, nullptr, n, stream);
+}
+
+int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                        uint32_t* d_verdict, uint32_t* d_flow_hash, size_t n, void* stream) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
@@ -2035,6 +2109,7 @@ int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
     a.cand_tile = c->cand_tile;
     a.stats = c->stats;
     a.stats_idx = c->stats_idx;
+    a.flow_hash = d_flow_hash;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     const size_t hist = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
     // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
@@ -2190,6 +2265,36 @@ int upe_gpu_diag_stamps(void* host, size_t bytes) {
     return 0;
 }
 #endif
+
+int upe_gpu_compact(upe_gpu_ctx_t* c, const uint32_t* d_verdict, size_t n, uint32_t code,
+                    uint32_t* d_index, uint64_t* d_count, void* stream) {
+    if (!c) return fail("null context");
+    if (!d_count || (n && (!d_verdict || !d_index))) return fail("null buffer");
+    if (n > 0xFFFFFFFFull - kCompactBlock) return fail("n must fit in 32 bits");
+    if (code > 15) return fail("verdict code out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(uint64_t), s));
+        return 0;
+    }
+    const uint32_t nb = (uint32_t)((n + kCompactBlock - 1) / kCompactBlock);
+    if (nb > c->compact_alloc) {
+        if (c->compact_counts) HIP_TRY(hipFree(c->compact_counts));
+        c->compact_counts = nullptr;
+        c->compact_alloc = 0;
+        HIP_TRY(hipMalloc(&c->compact_counts, nb * sizeof(uint32_t)));
+        c->compact_alloc = nb;
+    }
+    hipLaunchKernelGGL(upe_compact_count, dim3(nb), dim3(256), 0, s, d_verdict, (uint32_t)n, code,
+                       c->compact_counts);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(upe_compact_write, dim3(nb), dim3(256), 0, s, d_verdict, (uint32_t)n, code,
+                       c->compact_counts, nb, d_index,
+                       reinterpret_cast<unsigned long long*>(d_count));
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int upe_gpu_sync(upe_gpu_ctx_t* c, void* stream) {
     if (!c) return fail("null context");

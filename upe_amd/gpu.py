@@ -57,6 +57,8 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_memcpy_d2h": (I, [P, P, P, SZ, P]),
         "upe_gpu_process_host": (I, [P, P, SZ, P, P, SZ, SZ]),
         "upe_gpu_process_batches": (I, [P, P, P, P, SZ, SZ, P]),
+        "upe_gpu_process_rss": (I, [P, P, P, P, P, SZ, P]),
+        "upe_gpu_compact": (I, [P, P, SZ, ctypes.c_uint32, P, P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
     }
@@ -81,7 +83,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
-            "upe_gpu_process_batches", "upe_rules_load_ini", "upe_pcap_read",
+            "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
+            "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free")
 
@@ -189,6 +192,17 @@ class GpuWorker:
         _check(LIB.upe_gpu_process_batches(self._ctx, arr, _dev_ptr(desc), _dev_ptr(verdict), n,
                                            len(frames_ptrs), stream or None),
                "upe_gpu_process_batches")
+
+    def process_rss(self, frames, desc, verdict, flow_hash, n: int, stream=None) -> None:
+        """process() plus per-packet flow_hash (software RSS) into a device uint32 array."""
+        _check(LIB.upe_gpu_process_rss(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
+                                       _dev_ptr(verdict), _dev_ptr(flow_hash), n, stream or None),
+               "upe_gpu_process_rss")
+
+    def compact(self, verdict, n: int, code: int, index, count, stream=None) -> None:
+        """Indexes of the packets with verdict code `code`, in packet order (device buffers)."""
+        _check(LIB.upe_gpu_compact(self._ctx, _dev_ptr(verdict), n, code, _dev_ptr(index),
+                                   _dev_ptr(count), stream or None), "upe_gpu_compact")
 
     def sync(self, stream=None) -> None:
         _check(LIB.upe_gpu_sync(self._ctx, stream or None), "upe_gpu_sync")
