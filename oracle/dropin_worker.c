@@ -1,0 +1,212 @@
+/*
+ * oracle/dropin_worker.c — the MI355X path dropped into the REFERENCE pipeline.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Built by oracle/Makefile against the reference's own headers and
+ * sources where they lie (ring, pktbuf pool, rule table, neighbour tables, worker_init), into
+ * oracle/_ref/libupe_dropin.so (git-ignored), linked to this repo's libupe_gpu.so.
+ *
+ * What it shows: a reference worker_t, fed through the reference SPSC ring by an RX-like
+ * producer thread exactly as src/rx_pcap.c feeds it (pktbuf_alloc, memcpy, ring_push_burst),
+ * runs a GPU-backed worker loop instead of src/worker.c:255-307 — ring_pop_burst bursts
+ * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch, then
+ * the reference's TX accounting (tx_send_batch, pkts_forwarded / pkts_dropped, pktbuf_free) —
+ * and ends with the same counters and rule_stats in the same worker_t fields the reference's
+ * stats thread reads (src/main.c:293-315).  tests/test_gpu_dropin.py compares them with the
+ * reference worker itself (oracle/_ref/libupe_ref.so) on the same packets.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <signal.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "arp_table.h"
+#include "ndp_table.h"
+#include "pktbuf.h"
+#include "ring.h"
+#include "rule_table.h"
+#include "tx.h"
+#include "worker.h"
+
+#include "../include/upe_gpu.h"
+
+volatile sig_atomic_t g_stop = 0; /* defined by the program, reference src/main.c:27 */
+
+/* TX stubs, as reference tests/benchmark_throughput.c:30-42 */
+int tx_send(const tx_ctx_t *ctx, const uint8_t *frame, size_t len) {
+    (void)ctx; (void)frame; (void)len;
+    return 0;
+}
+int tx_send_batch(const tx_ctx_t *ctx, const uint8_t *const *frames, const size_t *lens, int count) {
+    (void)ctx; (void)frames; (void)lens;
+    return count;
+}
+
+#define GPU_BATCH 65536u
+#define WIN UPE_HDR_WINDOW
+
+typedef struct {
+    worker_t *w;
+    int device;
+    int rc;
+} gpu_arg_t;
+
+/* The TX flush of the reference worker loop, src/worker.c:286-303. */
+static void flush_tx(worker_t *w) {
+    if (w->tx_count > 0) {
+        int sent = tx_send_batch(w->tx, w->tx_frames, w->tx_lens, w->tx_count);
+        if (sent < 0) sent = 0;
+        w->pkts_forwarded += (uint64_t)sent;
+        w->pkts_dropped += (uint64_t)(w->tx_count - sent);
+        for (int i = 0; i < w->tx_count; i++) pktbuf_free(w->pool, w->tx_bufs[i]);
+        w->tx_count = 0;
+    }
+}
+
+/* GPU-backed replacement of worker_main (reference src/worker.c:255-307). */
+static void *gpu_worker_main(void *arg) {
+    gpu_arg_t *ga = arg;
+    worker_t *w = ga->w;
+    ga->rc = -1;
+    upe_gpu_ctx_t *ctx = upe_gpu_open(ga->device, w->rt->capacity);
+    uint8_t *win = upe_gpu_host_alloc((size_t)GPU_BATCH * WIN + UPE_FRAME_TAIL);
+    uint64_t *desc = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint64_t));
+    uint32_t *verdict = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint32_t));
+    pktbuf_t **bufs = malloc(GPU_BATCH * sizeof(*bufs));
+    if (!ctx || !win || !desc || !verdict || !bufs) return NULL;
+    if (upe_gpu_load_rules(ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
+        upe_gpu_load_neigh(ctx, (const upe_arp_entry_t *)w->arpt->entries, w->arpt->capacity,
+                           (const upe_ndp_entry_t *)w->ndpt->entries, w->ndpt->capacity) != 0 ||
+        upe_gpu_set_port(ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0)
+        return NULL;
+    size_t n = 0;
+    void *burst[WORKER_BURST_SIZE];
+    for (;;) {
+        unsigned k = ring_pop_burst(w->rx_ring, burst, WORKER_BURST_SIZE); /* worker.c:268 */
+        w->pkts_in += k;                                                   /* worker.c:280 */
+        for (unsigned j = 0; j < k; j++) {
+            pktbuf_t *b = burst[j];
+            size_t c = b->len < WIN ? b->len : WIN;
+            memcpy(win + n * WIN, b->data, c);
+            memset(win + n * WIN + c, 0, WIN - c);
+            desc[n] = UPE_DESC((uint64_t)n * WIN, b->len);
+            bufs[n++] = b;
+        }
+        const int stop = k == 0 && g_stop;
+        if (n == GPU_BATCH || (k == 0 && n > 0)) {
+            if (upe_gpu_process_host(ctx, win, (size_t)n * WIN + UPE_FRAME_TAIL, desc, verdict,
+                                     n, 0) != 0)
+                return NULL;
+            for (size_t i = 0; i < n; i++) {
+                pktbuf_t *b = bufs[i];
+                memcpy(b->data, win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
+                if (UPE_VERDICT_CODE(verdict[i]) == UPE_V_FWD) {
+                    w->tx_frames[w->tx_count] = b->data; /* worker.c:240-243 */
+                    w->tx_lens[w->tx_count] = b->len;
+                    w->tx_bufs[w->tx_count++] = b;
+                    if (w->tx_count == WORKER_BURST_SIZE) flush_tx(w);
+                } else if (UPE_VERDICT_CODE(verdict[i]) == UPE_V_CONSUMED) {
+                    pktbuf_free(w->pool, b); /* consumed control packet: no counter */
+                } else {
+                    w->pkts_dropped++; /* every drop path of process_packet counts one */
+                    pktbuf_free(w->pool, b);
+                }
+            }
+            flush_tx(w);
+            n = 0;
+        }
+        if (stop) break;
+    }
+    /* the counters the GPU keeps, into the reference's own worker_t fields */
+    upe_counters_t c;
+    if (upe_gpu_get_stats(ctx, &c, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity) != 0)
+        return NULL;
+    w->pkts_parsed = c.pkts_parsed;
+    w->pkts_matched = c.pkts_matched;
+    upe_gpu_host_free(win);
+    upe_gpu_host_free(desc);
+    upe_gpu_host_free(verdict);
+    free(bufs);
+    upe_gpu_close(ctx);
+    ga->rc = 0;
+    return NULL;
+}
+
+/*
+ * Run `n` packets (batch layout of include/upe_gpu.h) through: an RX-like producer thread ->
+ * reference SPSC ring -> reference worker_t driven by gpu_worker_main.  rules in insertion order
+ * (rule_table_add), neighbour slot arrays copied into reference tables.  Outputs the worker's
+ * counters (pkts_in, parsed, matched, forwarded, dropped) and rule_stats[capacity].
+ */
+int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
+                   const upe_arp_entry_t *arp, size_t arp_cap, const upe_ndp_entry_t *ndp,
+                   size_t ndp_cap, const uint8_t eth_addr[6], uint32_t ip4_addr,
+                   const uint8_t *frames, const uint64_t *in_desc, size_t n, int device,
+                   uint64_t counters[5], upe_rule_stat_t *rule_stats) {
+    rule_table_t rt;
+    if (rule_table_init(&rt, capacity) != 0) return -1;
+    for (size_t i = 0; i < nrules; i++)
+        if (rule_table_add(&rt, (const rule_t *)&rules[i]) != 0) return -1;
+    arp_table_t arpt;
+    ndp_table_t ndpt;
+    if (arp_table_init(&arpt, arp_cap ? arp_cap : 1) != 0 ||
+        ndp_table_init(&ndpt, ndp_cap ? ndp_cap : 1) != 0)
+        return -1;
+    if (arp_cap) memcpy(arpt.entries, arp, arp_cap * sizeof(arp_entry_t));
+    if (ndp_cap) memcpy(ndpt.entries, ndp, ndp_cap * sizeof(ndp_entry_t));
+    tx_ctx_t tx;
+    memset(&tx, 0, sizeof tx);
+    memcpy(tx.eth_addr, eth_addr, 6);
+    tx.ip4_addr = ip4_addr;
+    static pktbuf_pool_t pool; /* one pool per process (the TLS cache remembers it) */
+    static int pool_ready;
+    if (!pool_ready) {
+        if (pktbuf_pool_init(&pool, GPU_BATCH + 4096) != 0) return -1;
+        pool_ready = 1;
+    }
+    spsc_ring_t ring;
+    if (ring_init(&ring, 1024) != 0) return -1;
+    worker_t *w = calloc(1, sizeof(worker_t)); /* src/main.c:444 */
+    if (!w || worker_init(w, 0, -1, &ring, &pool, &rt, &tx, &arpt, &ndpt) != 0) return -1;
+
+    g_stop = 0;
+    gpu_arg_t ga = {w, device, -1};
+    pthread_t th;
+    pthread_create(&th, NULL, gpu_worker_main, &ga);
+    /* producer: the RX thread's copy-and-push, src/rx_pcap.c:42-93 (one ring, no RSS) */
+    void *staged[32];
+    unsigned ns = 0;
+    for (size_t i = 0; i < n; i++) {
+        pktbuf_t *b;
+        while (!(b = pktbuf_alloc(&pool))) { /* pool drained: wait for the worker to free */
+            struct timespec ts = {0, 1000};
+            nanosleep(&ts, NULL);
+        }
+        size_t off = (size_t)(in_desc[i] >> 16), len = (size_t)(in_desc[i] & 0xFFFF);
+        memset(b->data, 0, 128);
+        memcpy(b->data, frames + off, len);
+        b->len = len;
+        b->timestamp = 0;
+        staged[ns++] = b;
+        if (ns == 32 || i + 1 == n) {
+            unsigned done = 0;
+            while (done < ns) done += ring_push_burst(&ring, staged + done, ns - done);
+            ns = 0;
+        }
+    }
+    g_stop = 1;
+    pthread_join(th, NULL);
+    counters[0] = w->pkts_in;
+    counters[1] = w->pkts_parsed;
+    counters[2] = w->pkts_matched;
+    counters[3] = w->pkts_forwarded;
+    counters[4] = w->pkts_dropped;
+    if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
+    worker_destroy(w);
+    free(w);
+    ring_destroy(&ring);
+    arp_table_destroy(&arpt);
+    ndp_table_destroy(&ndpt);
+    rule_table_destroy(&rt);
+    return ga.rc;
+}

@@ -1,0 +1,54 @@
+"""The drop-in claim, tested: the REFERENCE pipeline (RX-like producer -> reference SPSC ring ->
+reference worker_t, built from the reference's sources by oracle/Makefile) running this repo's
+GPU worker loop (oracle/dropin_worker.c, the loop INTEGRATION.md shows) ends with the same
+worker counters and rule_stats as the reference's own src/worker.c on the same packets."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from upe_amd import synth
+from upe_amd.layout import RULE_STAT_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+SO = os.path.join(os.path.dirname(oracle.__file__), "_ref", "libupe_dropin.so")
+
+
+def _lib():
+    if not os.path.exists(SO):
+        pytest.fail(f"{SO} not built (make -C oracle where the reference sources exist)")
+    lib = ctypes.CDLL(SO)
+    P, SZ = ctypes.c_void_p, ctypes.c_size_t
+    lib.upe_dropin_run.restype = ctypes.c_int
+    lib.upe_dropin_run.argtypes = [P, SZ, SZ, P, SZ, P, SZ, P, ctypes.c_uint32, P, P, SZ,
+                                   ctypes.c_int, P, P]
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+@pytest.mark.parametrize("make", [lambda: synth.config_b(n=200_000, seed=61),
+                                  lambda: synth.config_c(n=100_000, seed=62)],
+                         ids=["B", "C"])
+def test_reference_pipeline_with_gpu_worker(make):
+    wl = make()
+    lib = _lib()
+    rules = np.ascontiguousarray(wl.rules)
+    eth = np.frombuffer(bytes(wl.eth_addr), np.uint8).copy()
+    counters = np.zeros(5, np.uint64)
+    stats = np.zeros(wl.capacity, RULE_STAT_DTYPE)
+    rc = lib.upe_dropin_run(_p(rules), len(rules), wl.capacity, _p(wl.arp), len(wl.arp),
+                            _p(wl.ndp), len(wl.ndp), _p(eth), wl.ip4_addr, _p(wl.frames),
+                            _p(wl.desc), wl.n, 0, _p(counters), _p(stats))
+    assert rc == 0
+    ref = oracle.run_reference(wl)
+    want = [int(x) for x in ref.counters[0].tolist()[:5]]
+    assert [int(x) for x in counters] == want
+    assert np.array_equal(stats, ref.rule_stats)
