@@ -158,11 +158,27 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     memset(&tx, 0, sizeof tx);
     memcpy(tx.eth_addr, eth_addr, 6);
     tx.ip4_addr = ip4_addr;
-    static pktbuf_pool_t pool; /* one pool per process (the TLS cache remembers it) */
-    static int pool_ready;
-    if (!pool_ready) {
-        if (pktbuf_pool_init(&pool, GPU_BATCH + 4096) != 0) return -1;
-        pool_ready = 1;
+    /* One pool per process (the pool's thread-local caches remember it), sized so that every
+     * packet of the run gets its own buffer: the producer allocates all of them before the
+     * worker frees any, so the test does not lean on concurrent alloc/free in the pool. */
+    static pktbuf_pool_t pool;
+    static size_t pool_cap;
+    if (pool_cap < n + 256) {
+        if (pool_cap) return -1; /* one size per process */
+        if (pktbuf_pool_init(&pool, n + 256) != 0) return -1;
+        pool_cap = n + 256;
+    }
+    pktbuf_t **all = malloc((n ? n : 1) * sizeof(*all));
+    if (!all) return -1;
+    for (size_t i = 0; i < n; i++) {
+        pktbuf_t *b = pktbuf_alloc(&pool);
+        if (!b) return -1;
+        size_t off = (size_t)(in_desc[i] >> 16), len = (size_t)(in_desc[i] & 0xFFFF);
+        memset(b->data, 0, 128);
+        memcpy(b->data, frames + off, len);
+        b->len = len;
+        b->timestamp = 0;
+        all[i] = b;
     }
     spsc_ring_t ring;
     if (ring_init(&ring, 1024) != 0) return -1;
@@ -173,26 +189,10 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     gpu_arg_t ga = {w, device, -1};
     pthread_t th;
     pthread_create(&th, NULL, gpu_worker_main, &ga);
-    /* producer: the RX thread's copy-and-push, src/rx_pcap.c:42-93 (one ring, no RSS) */
-    void *staged[32];
-    unsigned ns = 0;
-    for (size_t i = 0; i < n; i++) {
-        pktbuf_t *b;
-        while (!(b = pktbuf_alloc(&pool))) { /* pool drained: wait for the worker to free */
-            struct timespec ts = {0, 1000};
-            nanosleep(&ts, NULL);
-        }
-        size_t off = (size_t)(in_desc[i] >> 16), len = (size_t)(in_desc[i] & 0xFFFF);
-        memset(b->data, 0, 128);
-        memcpy(b->data, frames + off, len);
-        b->len = len;
-        b->timestamp = 0;
-        staged[ns++] = b;
-        if (ns == 32 || i + 1 == n) {
-            unsigned done = 0;
-            while (done < ns) done += ring_push_burst(&ring, staged + done, ns - done);
-            ns = 0;
-        }
+    /* producer: the RX thread's staged bursts of 32 into the ring, src/rx_pcap.c:80-92 */
+    for (size_t i = 0; i < n; i += 32) {
+        unsigned ns = (unsigned)(n - i < 32 ? n - i : 32), done = 0;
+        while (done < ns) done += ring_push_burst(&ring, (void **)(all + i) + done, ns - done);
     }
     g_stop = 1;
     pthread_join(th, NULL);
@@ -204,6 +204,7 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
     worker_destroy(w);
     free(w);
+    free(all);
     ring_destroy(&ring);
     arp_table_destroy(&arpt);
     ndp_table_destroy(&ndpt);

@@ -34,8 +34,8 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-@pytest.mark.parametrize("make", [lambda: synth.config_b(n=200_000, seed=61),
-                                  lambda: synth.config_c(n=100_000, seed=62)],
+@pytest.mark.parametrize("make", [lambda: synth.config_b(n=150_000, seed=61),
+                                  lambda: synth.config_c(n=150_000, seed=62)],
                          ids=["B", "C"])
 def test_reference_pipeline_with_gpu_worker(make):
     wl = make()
