@@ -189,7 +189,9 @@ def main() -> None:
 
     fbytes = int(wl.frames.nbytes)
     stride = (fbytes + 255) // 256 * 256
-    copies = min(args.steps + args.warmup, args.max_copies)
+    # distinct copies of the batch, so no step finds its frames in a cache a previous step
+    # warmed (bounded to 64 GiB of HBM: config D's 2 GiB batch gets 32)
+    copies = max(2, min(args.steps + args.warmup, args.max_copies, (64 << 30) // stride))
     pristine = torch.from_numpy(wl.frames).to(dev)
     pool = torch.empty(copies * stride, dtype=torch.uint8, device=dev)
     for c in range(copies):
