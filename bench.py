@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-EVENT_EVERY = 8   # sample the kernel events on every 8th timed step
+EVENT_EVERY = 20  # sample the kernel events on every 20th timed step (10 samples at K=200)
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
 WORKLOADS = {
     "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",

@@ -263,6 +263,23 @@ int upe_gpu_process_rss(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d
 int upe_gpu_compact(upe_gpu_ctx_t *ctx, const uint32_t *d_verdict, size_t n, uint32_t code,
                     uint32_t *d_index, uint64_t *d_count, void *stream);
 
+/* A batch with exact control-packet semantics, as the reference's burst loop runs it
+ * (src/worker.c:23-104 inside process_packet): an ARP packet with the Ethernet/IPv4 header, or
+ * an NDP NS/NA carrying a link-layer address option, writes a neighbour table, and every later
+ * packet sees the new entry.  The batch is cut after each such packet: the segment up to and
+ * including it runs as upe_gpu_process(), its write — arp_update(spa, sha)
+ * (src/arp_table.c:26-53) or ndp_update(src | target, lladdr) (src/ndp_table.c:39-65, option
+ * walk src/worker.c:68-95) — is applied to the caller's host slot arrays `arp` / `ndp` (the
+ * ones last given to upe_gpu_load_neigh; updated in place, update_at = now, as the reference's
+ * tables are), the new snapshot is uploaded, and the next segment runs.  Control packets are
+ * found on the device (one marking pass plus an ordered compaction), so a batch without them
+ * costs one extra pass.  Synchronous; *n_writes (optional) = table writes applied.  Capacities
+ * are powers of two, as arp_table_init / ndp_table_init require. */
+int upe_gpu_process_segmented(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                              uint32_t *d_verdict, size_t n, upe_arp_entry_t *arp,
+                              size_t arp_capacity, upe_ndp_entry_t *ndp, size_t ndp_capacity,
+                              int64_t now, size_t *n_writes, void *stream);
+
 /* Wait for all work queued on the context's stream (or `stream`). */
 int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
 

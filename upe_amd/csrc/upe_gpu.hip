@@ -1397,6 +1397,45 @@ uint32_t mac_lo(const uint8_t* m) {
 uint32_t mac_hi(const uint8_t* m) { return (uint32_t)m[4] | ((uint32_t)m[5] << 8); }
 uint32_t le32(const uint8_t* p) { return mac_lo(p); }
 
+// ------------------------------------------------------------------------------------------
+// Control packets that write a neighbour table (upe_gpu_process_segmented).  A packet is
+// marked when handle_control_packet (reference src/worker.c:23-104) may call arp_update or
+// ndp_update for it: ARP with the Ethernet/IPv4 header (the learn does not look at len), or an
+// IPv6 NS/NA of at least 78 bytes (whether an option carries the address is decided on the
+// host, from the gathered bytes).  Bytes at or past len read as zero (zero-filled pktbuf).
+// Marks are verdict-shaped words (code 1 = marked) so upe_compact_* lists them in order.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kCtrlWin = 256;   // bytes of each marked frame gathered for the host
+
+__global__ void __launch_bounds__(256) upe_ctrl_mark(const uint8_t* frames, const uint64_t* desc,
+                                                     uint32_t n, uint32_t* marks) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t d = desc[i];
+    const uint32_t len = (uint32_t)(d & 0xFFFFu);
+    const uint8_t* p = frames + (d >> 16);
+    auto at = [&](uint32_t k) -> uint32_t { return k < len ? (uint32_t)p[k] : 0u; };
+    const uint32_t et = at(12) << 8 | at(13);
+    uint32_t m = 0;
+    if (et == 0x0806)
+        m = at(14) == 0 && at(15) == 1 && at(16) == 8 && at(17) == 0 && at(18) == 6 && at(19) == 4;
+    else if (et == 0x86DD && len >= 78u && at(20) == 58u && (at(54) == 135u || at(54) == 136u))
+        m = 1;
+    marks[i] = m;
+}
+
+// One workgroup per marked packet: its first kCtrlWin bytes (zero past len) and its length.
+__global__ void __launch_bounds__(256) upe_ctrl_gather(const uint8_t* frames, const uint64_t* desc,
+                                                       const uint32_t* index, uint8_t* win,
+                                                       uint32_t* lens) {
+    const uint32_t i = index[blockIdx.x];
+    const uint64_t d = desc[i];
+    const uint32_t len = (uint32_t)(d & 0xFFFFu);
+    const uint32_t k = threadIdx.x;
+    win[(size_t)blockIdx.x * kCtrlWin + k] = k < len ? frames[(d >> 16) + k] : (uint8_t)0;
+    if (k == 0) lens[blockIdx.x] = len;
+}
+
 }  // namespace
 
 struct upe_gpu_ctx {
@@ -1420,6 +1459,14 @@ struct upe_gpu_ctx {
     bool tss = false;
     uint32_t* compact_counts = nullptr;   // upe_gpu_compact: per-block counts
     size_t compact_alloc = 0;
+    // upe_gpu_process_segmented scratch: marks / index [ctrl_alloc], gathered windows
+    uint32_t* ctrl_marks = nullptr;
+    uint32_t* ctrl_index = nullptr;
+    uint64_t* ctrl_count = nullptr;
+    size_t ctrl_alloc = 0;
+    uint8_t* ctrl_win = nullptr;
+    uint32_t* ctrl_lens = nullptr;
+    size_t ctrl_win_alloc = 0;
     // neighbour tables (reachable-entry indexes)
     uint4* arp = nullptr;
     uint32_t arp_bits = 0, arp_seed = 0;
@@ -1659,7 +1706,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->compact_counts};
+                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->compact_counts,
+                    c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -2293,6 +2341,169 @@ int upe_gpu_compact(upe_gpu_ctx_t* c, const uint32_t* d_verdict, size_t n, uint3
                        c->compact_counts, nb, d_index,
                        reinterpret_cast<unsigned long long*>(d_count));
     HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// The table writes of handle_control_packet, restated on the caller's host slot arrays.
+// arp_update, reference src/arp_table.c:26-53: home slot ip & (cap-1), linear probe, insert at
+// the first free slot or update the slot holding ip, at most cap probes.
+void host_arp_update(upe_arp_entry_t* t, size_t cap, uint32_t ip, const uint8_t* mac,
+                     int64_t now) {
+    const size_t idx = ip & (cap - 1);
+    for (size_t k = 0; k < cap; ++k) {
+        upe_arp_entry_t& e = t[(idx + k) & (cap - 1)];
+        if (!e.valid || e.ip == ip) {
+            if (!e.valid) {
+                e.valid = true;
+                e.ip = ip;
+            }
+            memcpy(e.mac, mac, 6);
+            e.update_at = now;
+            return;
+        }
+    }
+}
+
+// ndp_update, reference src/ndp_table.c:39-65 (hash_ipv6 :6-17: XOR of the address's four
+// native-endian words, & (cap-1)).
+void host_ndp_update(upe_ndp_entry_t* t, size_t cap, const uint8_t* ip, const uint8_t* mac,
+                     int64_t now) {
+    const uint32_t h = le32(ip) ^ le32(ip + 4) ^ le32(ip + 8) ^ le32(ip + 12);
+    const size_t idx = h & (cap - 1);
+    for (size_t k = 0; k < cap; ++k) {
+        upe_ndp_entry_t& e = t[(idx + k) & (cap - 1)];
+        if (!e.valid || memcmp(e.ip, ip, 16) == 0) {
+            if (!e.valid) {
+                e.valid = true;
+                memcpy(e.ip, ip, 16);
+            }
+            memcpy(e.mac, mac, 6);
+            e.update_at = now;
+            return;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                              uint32_t* d_verdict, size_t n, upe_arp_entry_t* arp,
+                              size_t arp_capacity, upe_ndp_entry_t* ndp, size_t ndp_capacity,
+                              int64_t now, size_t* n_writes, void* stream) {
+    if (!c) return fail("null context");
+    if (n_writes) *n_writes = 0;
+    if (n > 0xFFFFFFFFull - kCompactBlock) return fail("batch too large (n must fit in 32 bits)");
+    if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
+    if ((arp_capacity && !arp) || (ndp_capacity && !ndp)) return fail("null neighbour table");
+    if ((arp_capacity & (arp_capacity - 1)) || (ndp_capacity & (ndp_capacity - 1)))
+        return fail("neighbour table capacities must be powers of two");
+    if (n == 0) return upe_gpu_process(c, d_frames, d_desc, d_verdict, 0, stream);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    // 1. mark and list the table-writing control packets, in packet order
+    if (n > c->ctrl_alloc) {
+        for (void* b : {(void*)c->ctrl_marks, (void*)c->ctrl_index})
+            if (b) HIP_TRY(hipFree(b));
+        c->ctrl_marks = c->ctrl_index = nullptr;
+        c->ctrl_alloc = 0;
+        HIP_TRY(hipMalloc(&c->ctrl_marks, n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&c->ctrl_index, n * sizeof(uint32_t)));
+        if (!c->ctrl_count) HIP_TRY(hipMalloc(&c->ctrl_count, sizeof(uint64_t)));
+        c->ctrl_alloc = n;
+    }
+    hipLaunchKernelGGL(upe_ctrl_mark, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       d_frames, d_desc, (uint32_t)n, c->ctrl_marks);
+    HIP_TRY(hipGetLastError());
+    if (upe_gpu_compact(c, c->ctrl_marks, n, 1u, c->ctrl_index, c->ctrl_count, s) != 0) return -1;
+    uint64_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, c->ctrl_count, sizeof cnt, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (cnt == 0) return upe_gpu_process(c, d_frames, d_desc, d_verdict, n, stream);
+    // 2. their bytes, gathered before any segment runs (the ARP reply is built in place)
+    if (cnt > c->ctrl_win_alloc) {
+        for (void* b : {(void*)c->ctrl_win, (void*)c->ctrl_lens})
+            if (b) HIP_TRY(hipFree(b));
+        c->ctrl_win = nullptr;
+        c->ctrl_lens = nullptr;
+        c->ctrl_win_alloc = 0;
+        HIP_TRY(hipMalloc(&c->ctrl_win, cnt * kCtrlWin));
+        HIP_TRY(hipMalloc(&c->ctrl_lens, cnt * sizeof(uint32_t)));
+        c->ctrl_win_alloc = cnt;
+    }
+    hipLaunchKernelGGL(upe_ctrl_gather, dim3((uint32_t)cnt), dim3(kCtrlWin), 0, s, d_frames,
+                       d_desc, c->ctrl_index, c->ctrl_win, c->ctrl_lens);
+    HIP_TRY(hipGetLastError());
+    std::vector<uint32_t> idx(cnt), lens(cnt);
+    std::vector<uint8_t> win(cnt * kCtrlWin);
+    HIP_TRY(hipMemcpyAsync(idx.data(), c->ctrl_index, cnt * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(lens.data(), c->ctrl_lens, cnt * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(win.data(), c->ctrl_win, win.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // 3. segments: up to and including each control packet, then its table write
+    size_t start = 0, writes = 0;
+    std::vector<uint8_t> full;
+    for (uint64_t j = 0; j < cnt; ++j) {
+        const size_t k = idx[j];
+        if (upe_gpu_process(c, d_frames, d_desc + start, d_verdict + start, k + 1 - start,
+                            stream) != 0)
+            return -1;
+        start = k + 1;
+        const uint8_t* b = win.data() + j * kCtrlWin;
+        const uint32_t len = lens[j];
+        bool wrote = false;
+        if (b[12] == 0x08 && b[13] == 0x06) {
+            // ARP learn, src/worker.c:30-39: spa (network order) -> host order, sha
+            if (arp_capacity) {
+                const uint32_t spa = (uint32_t)b[28] << 24 | (uint32_t)b[29] << 16 |
+                                     (uint32_t)b[30] << 8 | (uint32_t)b[31];
+                host_arp_update(arp, arp_capacity, spa, b + 22, now);
+                wrote = true;
+            }
+        } else {
+            // NS / NA option walk, src/worker.c:64-95, over the whole frame when it is long
+            const uint8_t* f = b;
+            if (len > kCtrlWin) {
+                uint64_t d = 0;
+                HIP_TRY(hipMemcpy(&d, d_desc + k, sizeof d, hipMemcpyDeviceToHost));
+                full.assign(len, 0);
+                HIP_TRY(hipMemcpy(full.data(), d_frames + (d >> 16), len, hipMemcpyDeviceToHost));
+                f = full.data();
+            }
+            const bool ns = f[54] == 135;
+            for (size_t off = 78; off + 2 <= len;) {
+                const uint32_t ot = f[off], ol = (uint32_t)f[off + 1] * 8u;
+                if (ol == 0 || off + ol > len) break;
+                if (ol >= 8 && ((ns && ot == 1) || (!ns && ot == 2))) {
+                    if (ndp_capacity) {
+                        host_ndp_update(ndp, ndp_capacity, ns ? f + 22 : f + 62, f + off + 2, now);
+                        wrote = true;
+                    }
+                    break;
+                }
+                off += ol;
+            }
+        }
+        if (wrote) {
+            ++writes;
+            // the next segment reads the new snapshot (load_neigh waits for the context's
+            // stream; a caller stream is drained first)
+            if (s != c->stream) HIP_TRY(hipStreamSynchronize(s));
+            if (upe_gpu_load_neigh(c, arp, arp_capacity, ndp, ndp_capacity) != 0) return -1;
+        }
+    }
+    if (start < n &&
+        upe_gpu_process(c, d_frames, d_desc + start, d_verdict + start, n - start, stream) != 0)
+        return -1;
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n_writes) *n_writes = writes;
     return 0;
 }
 

@@ -59,6 +59,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_batches": (I, [P, P, P, P, SZ, SZ, P]),
         "upe_gpu_process_rss": (I, [P, P, P, P, P, SZ, P]),
         "upe_gpu_compact": (I, [P, P, SZ, ctypes.c_uint32, P, P, P]),
+        "upe_gpu_process_segmented": (I, [P, P, P, P, SZ, P, SZ, P, SZ, ctypes.c_int64, P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
     }
@@ -84,6 +85,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
+            "upe_gpu_process_segmented",
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free")
@@ -198,6 +200,20 @@ class GpuWorker:
         _check(LIB.upe_gpu_process_rss(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
                                        _dev_ptr(verdict), _dev_ptr(flow_hash), n, stream or None),
                "upe_gpu_process_rss")
+
+    def process_segmented(self, frames, desc, verdict, n: int, arp: np.ndarray,
+                          ndp: np.ndarray, now: int = 0, stream=None) -> int:
+        """A device batch with exact control-packet semantics: cut after every table-writing
+        ARP / NS / NA packet, apply the write to `arp` / `ndp` (host slot arrays, updated in
+        place) and upload them again.  Returns the number of table writes."""
+        assert arp.dtype == ARP_DTYPE and ndp.dtype == NDP_DTYPE
+        assert arp.flags.c_contiguous and ndp.flags.c_contiguous
+        nw = ctypes.c_size_t(0)
+        _check(LIB.upe_gpu_process_segmented(
+            self._ctx, _dev_ptr(frames), _dev_ptr(desc), _dev_ptr(verdict), n,
+            _np_ptr(arp) if len(arp) else None, len(arp), _np_ptr(ndp) if len(ndp) else None,
+            len(ndp), now, ctypes.byref(nw), stream or None), "upe_gpu_process_segmented")
+        return nw.value
 
     def compact(self, verdict, n: int, code: int, index, count, stream=None) -> None:
         """Indexes of the packets with verdict code `code`, in packet order (device buffers)."""
