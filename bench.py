@@ -31,7 +31,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-EVENT_EVERY = 20  # sample the kernel events on every 20th timed step (10 samples at K=200)
+EVENT_EVERY = 20  # open a kernel-timing sample on every 20th timed step (10 samples at K=200)
+EVENT_SPAN = 5    # each sample's HIP event pair brackets 5 consecutive launches
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
 WORKLOADS = {
     "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",
@@ -63,6 +64,43 @@ def algorithmic_bytes(wl, verdict: np.ndarray) -> np.ndarray:
     hit = (verdict & 0x10) != 0
     W = np.where(fwd & is4, 3, 0) + np.where(fwd & is6, 1, 0) + np.where(fwd & hit, 12, 0)
     return 8 + E + 4 + W
+
+
+def rule_evals(wl, verdict: np.ndarray) -> int:
+    """Rule tests the reference's linear first-match scan makes on this batch
+    (src/rule_table.c:163-176): first-match position for matched packets, the whole table for
+    parsed packets that match nothing, none for parse failures."""
+    code = verdict & 0xF
+    rule = (verdict >> 8).astype(np.int64)   # sorted index + 1, 0 = no match
+    parsed = (code != 0) & (code != 5)
+    return int(np.where(rule > 0, rule, np.where(parsed, len(wl.rules), 0)).sum())
+
+
+def hbm_probe(torch, dev, gib: int = 4, reps: int = 10) -> dict:
+    """Achievable HBM streaming rates on this GPU (SURVEY.md §8(d) asks for them beside the
+    nominal 8 TB/s): a device-to-device copy and a read-only reduction over `gib` GiB buffers,
+    timed with HIP events; outside the timed region."""
+    n = gib << 30
+    a = torch.ones(n // 8, dtype=torch.int64, device=dev)
+    b = torch.empty_like(a)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    b.copy_(a)
+    a.sum()
+    torch.cuda.synchronize(dev)
+    ev[0].record()
+    for _ in range(reps):
+        b.copy_(a)
+    ev[1].record()
+    for _ in range(reps):
+        a.sum()
+    ev[2].record()
+    torch.cuda.synchronize(dev)
+    t_copy = ev[0].elapsed_time(ev[1]) / 1e3
+    t_read = ev[1].elapsed_time(ev[2]) / 1e3
+    del a, b
+    return {"copy_GBps": round(2 * n * reps / t_copy / 1e9, 1),
+            "read_GBps": round(n * reps / t_read / 1e9, 1),
+            "method": f"torch copy_ (read + write) and sum (read) over {gib} GiB, HIP events"}
 
 
 def pmc_traffic(config: str, packets: int):
@@ -155,6 +193,8 @@ def main() -> None:
                          "rocprof summary of the default command holds only full-batch "
                          "launches; DESIGN.md quotes a --host-reps 10 run)")
     ap.add_argument("--host-chunk", type=int, default=0)
+    ap.add_argument("--no-hbm-probe", action="store_true",
+                    help="skip the achievable-bandwidth probe (copy / read kernels)")
     args = ap.parse_args()
 
     import torch
@@ -210,11 +250,14 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     v_first = verdict.cpu().numpy().view(np.uint32).copy()  # warm-up batch 0 verdicts
 
-    # Kernel timing events ride along in the timed region on every EVENT_EVERY-th step: each
-    # event is a queue packet of its own (a few us), so timing every step would tax the very
-    # throughput being measured.  UPE_BENCH_EVENTS=0: diagnostic run without them.
+    # Kernel timing events ride along in the timed region: a sample opens on every
+    # EVENT_EVERY-th step and its event pair brackets EVENT_SPAN consecutive launches.  Each
+    # event is a queue packet of its own (a few us of latency), so an event pair around every
+    # launch would both tax the throughput being measured and inflate the per-launch time; over
+    # 5 launches the pair's latency is spread thin (the gaps between those launches remain in
+    # the time).  UPE_BENCH_EVENTS=0: diagnostic run without them.
     events = os.environ.get("UPE_BENCH_EVENTS", "1") != "0"
-    worker.timing_enable(EVENT_EVERY if events else 0)
+    worker.timing_span(EVENT_EVERY if events else 0, EVENT_SPAN)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -226,6 +269,7 @@ def main() -> None:
     t1 = time.perf_counter()
     classify_ms, finalize_ms, launches = worker.timing_read()
     worker.timing_enable(False)
+    probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
     worker.reset_stats()
@@ -281,6 +325,16 @@ def main() -> None:
                 "algorithmic_bytes_per_packet": round(bytes_per_launch / n, 2),
                 "kernel_mpps": round(n / kern_s / 1e6, 1),
                 "event_samples": int(launches),
+                "achievable": probe,
+                "frac_of_achievable_read": (round(achieved / probe["read_GBps"], 4)
+                                            if probe else None),
+            },
+            "rule_scan_equiv": {
+                "evals_per_batch": rule_evals(wl, v_first),
+                "G_evals_per_s": round(rule_evals(wl, v_first) * args.steps * world / elapsed
+                                       / 1e9, 2),
+                "what": "rule tests the reference's linear first-match scan would make on these "
+                        "batches (src/rule_table.c:163-176) / wall time",
             },
         }
         if hr:

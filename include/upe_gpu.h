@@ -292,11 +292,15 @@ int upe_gpu_get_stats(upe_gpu_ctx_t *ctx, upe_counters_t *counters, upe_rule_sta
 int upe_gpu_reset_stats(upe_gpu_ctx_t *ctx);
 
 /* Kernel timing.  enable = k > 0: every k-th upe_gpu_process() call (the first, then every k-th)
- * records HIP events on its stream around each of its two launches (classify: one workgroup per
- * 256-packet tile; finalize: the batch-wide fold); sampling keeps the events' own queue cost out
- * of a throughput run.  enable = 0 turns timing off.  upe_gpu_timing_read() synchronises and
- * returns the summed time (ms) of each kernel over the timed calls and their number. */
+ * records HIP events on its stream around its launches (classify, plus the rule_stats group-by
+ * pass of tables over 4096 rules); sampling keeps the events' own queue cost out of a throughput
+ * run.  enable = 0 turns timing off.  upe_gpu_timing_span(ctx, every, span): each sample's
+ * event pair brackets `span` consecutive calls instead of one, so the events' own latency is
+ * spread over `span` launches (the time then includes the gaps between those launches).
+ * upe_gpu_timing_read() synchronises and returns the summed time (ms) of the closed samples and
+ * the number of calls they cover (finalize_ms is 0: the fold runs inside the classify launch). */
 int upe_gpu_timing_enable(upe_gpu_ctx_t *ctx, int enable);
+int upe_gpu_timing_span(upe_gpu_ctx_t *ctx, int every, int span);
 int upe_gpu_timing_read(upe_gpu_ctx_t *ctx, double *classify_ms, double *finalize_ms,
                         uint64_t *launches);
 

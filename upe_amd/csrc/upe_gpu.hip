@@ -1494,6 +1494,9 @@ struct upe_gpu_ctx {
     // kernel timing (upe_gpu_timing_*)
     bool timing = false;
     uint32_t timing_every = 1, timing_calls = 0;   // sample every n-th process() call
+    uint32_t timing_span = 1;      // calls one sample's event pair brackets
+    uint32_t t_left = 0;           // calls left in the open sample (0: none open)
+    uint64_t timing_launches = 0;  // calls covered by closed samples
     std::vector<hipEvent_t> ev;   // event pool, 2 per timed process() call
     size_t ev_used = 0;
     // host round trip (upe_gpu_process_host): copy streams and three device slots
@@ -2118,17 +2121,18 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
         HIP_TRY(hipStreamWaitEvent(s, dep, 0));
         HIP_TRY(hipEventDestroy(dep));
     }
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    const bool timed = c->timing && (c->timing_calls++ % c->timing_every) == 0;
-    if (timed) {
+    // timing sample: an event pair around `timing_span` consecutive calls, opened on every
+    // timing_every-th call (samples never overlap)
+    const bool open = c->timing && c->t_left == 0 && (c->timing_calls % c->timing_every) == 0;
+    if (c->timing) ++c->timing_calls;
+    if (open) {
         while (c->ev.size() < c->ev_used + 2) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             c->ev.push_back(e);
         }
-        for (int j = 0; j < 2; ++j) ev[j] = c->ev[c->ev_used + j];
-        c->ev_used += 2;
-        HIP_TRY(hipEventRecord(ev[0], s));
+        HIP_TRY(hipEventRecord(c->ev[c->ev_used], s));
+        c->t_left = c->timing_span;
     }
     Args a;
     a.frames = d_frames;
@@ -2189,7 +2193,11 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
                            c->nrules_pad, c->stats_idx);
         HIP_TRY(hipGetLastError());
     }
-    if (timed) HIP_TRY(hipEventRecord(ev[1], s));
+    if (c->t_left && --c->t_left == 0) {
+        HIP_TRY(hipEventRecord(c->ev[c->ev_used + 1], s));
+        c->ev_used += 2;
+        c->timing_launches += c->timing_span;
+    }
     c->have_batch = true;
     return 0;
 }
@@ -2577,15 +2585,23 @@ int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
     return 0;
 }
 
-int upe_gpu_timing_enable(upe_gpu_ctx_t* c, int enable) {
+int upe_gpu_timing_span(upe_gpu_ctx_t* c, int every, int span) {
     if (!c) return fail("null context");
+    if (span < 1) return fail("span must be at least 1");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
     c->ev_used = 0;   // the pool is kept for reuse
-    c->timing = enable > 0;
-    c->timing_every = enable > 0 ? (uint32_t)enable : 1u;
+    c->timing = every > 0;
+    c->timing_every = every > 0 ? (uint32_t)every : 1u;
+    c->timing_span = (uint32_t)span;
     c->timing_calls = 0;
+    c->t_left = 0;
+    c->timing_launches = 0;
     return 0;
+}
+
+int upe_gpu_timing_enable(upe_gpu_ctx_t* c, int enable) {
+    return upe_gpu_timing_span(c, enable, 1);
 }
 
 int upe_gpu_timing_read(upe_gpu_ctx_t* c, double* classify_ms, double* finalize_ms,
@@ -2601,7 +2617,7 @@ int upe_gpu_timing_read(upe_gpu_ctx_t* c, double* classify_ms, double* finalize_
     }
     if (classify_ms) *classify_ms = a;
     if (finalize_ms) *finalize_ms = b;
-    if (launches) *launches = c->ev_used / 2;
+    if (launches) *launches = c->timing_launches;
     return 0;
 }
 

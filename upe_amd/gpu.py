@@ -50,6 +50,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_get_stats": (I, [P, P, P, SZ]),
         "upe_gpu_reset_stats": (I, [P]),
         "upe_gpu_timing_enable": (I, [P, I]),
+        "upe_gpu_timing_span": (I, [P, I, I]),
         "upe_gpu_timing_read": (I, [P, P, P, P]),
         "upe_gpu_malloc": (P, [P, SZ]),
         "upe_gpu_free": (I, [P, P]),
@@ -82,6 +83,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
             "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
+            "upe_gpu_timing_span",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
@@ -242,6 +244,11 @@ class GpuWorker:
     def timing_enable(self, every: int = 1) -> None:
         """Record kernel events on every ``every``-th process() call (0 / False: off)."""
         _check(LIB.upe_gpu_timing_enable(self._ctx, int(every)), "upe_gpu_timing_enable")
+
+    def timing_span(self, every: int, span: int) -> None:
+        """Each sample's event pair brackets ``span`` consecutive calls, one sample opened on
+        every ``every``-th call."""
+        _check(LIB.upe_gpu_timing_span(self._ctx, int(every), int(span)), "upe_gpu_timing_span")
 
     def timing_read(self):
         a, b = ctypes.c_double(), ctypes.c_double()
