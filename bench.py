@@ -248,7 +248,6 @@ def main() -> None:
 
     steps(0, args.warmup)
     torch.cuda.synchronize(dev)
-    v_first = verdict.cpu().numpy().view(np.uint32).copy()  # warm-up batch 0 verdicts
 
     # Kernel timing events ride along in the timed region: a sample opens on every
     # EVENT_EVERY-th step and its event pair brackets EVENT_SPAN consecutive launches.  Each
@@ -262,11 +261,27 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    steps(args.warmup, args.steps)
+    if os.environ.get("UPE_BENCH_TRACE"):
+        # diagnostic: where the host time of the timed region goes
+        steps(args.warmup, 1)
+        ta = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        tb = time.perf_counter()
+        steps(args.warmup + 1, args.steps - 1)
+        tc = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        print(f"trace: first call {1e3 * (ta - t0):.3f} ms, its sync {1e3 * (tb - ta):.3f} ms, "
+              f"rest queued {1e3 * (tc - tb):.3f} ms, rest sync {1e3 * (time.perf_counter() - tc):.3f}"
+              " ms", file=sys.stderr)
+    else:
+        steps(args.warmup, args.steps)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
+    # the last batch's verdicts (every step has the same packets): the basis of the algorithmic
+    # bytes.  Read after the timed region: a large D2H before it delayed the first timed launch.
+    v_first = verdict.cpu().numpy().view(np.uint32).copy()
     classify_ms, finalize_ms, launches = worker.timing_read()
     worker.timing_enable(False)
     probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
