@@ -201,13 +201,20 @@ def main() -> None:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them round robin
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL ("nccl") carries only the barrier and the max / sum over ranks; the gloo backend
+        # (UPE_BENCH_DIST_BACKEND=gloo) rehearses the multi-rank path on a one-GPU box
+        backend = os.environ.get("UPE_BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -365,7 +372,7 @@ def main() -> None:
                         "header bytes, 3-slot pipeline (upe_gpu_process_host); median of "
                         f"{hr['reps']} passes, all ranks at once",
             }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
         print(json.dumps(out), flush=True)
     worker.close()

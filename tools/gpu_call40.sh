@@ -1,0 +1,3 @@
+bash tools/gpu_session.sh \
+ "dist2:300:UPE_BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5" \
+ "dist4C:300:UPE_BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --config C --steps 50 --warmup 5 --no-hbm-probe"
