@@ -82,9 +82,6 @@ constexpr uint32_t kArpLdsSlots = 1024;   // ARP indexes up to 16 KB are staged 
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kShards = 8;             // arrival-ticket shards
-#ifndef UPE_GLDS
-#define UPE_GLDS 0   // header windows by LDS-DMA (0: per-lane 16-byte loads, for A/B timing)
-#endif
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
@@ -824,9 +821,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_last;    // this workgroup arrived last (set by wave 0)
-#if UPE_GLDS
-    __shared__ uint4 s_win[kWaves][256];   // per wave: 64 frames x bytes 0..63 (LDS-DMA target)
-#endif
 
     if (kAblate & 64) return;
     STAMP(0);
@@ -892,39 +886,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint32_t w[20];
 #pragma unroll
         for (int j = 0; j < 20; ++j) w[j] = 0;
-#if UPE_GLDS
-        {
-            // Bytes 0..63 of the wave's 64 frames arrive by LDS-DMA in four fully coalesced
-            // wave-instructions (16 frames x 64 B each, contiguous for packed frames), not as
-            // 64-byte-strided per-lane loads: each line leaves L2 once.  Slot P of this wave's
-            // window holds chunk (P & 3) ^ ((P >> 4) & 3) of frame P >> 2, so that the per-lane
-            // read-back below is free of LDS bank conflicts.
-            const uint32_t wbase = tile * kTile + (uint32_t)wave * 64u;
-            const uint8_t* fr = a.frames;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int P = 64 * k + lane;
-                const int j = P >> 2;
-                const int c = (P & 3) ^ ((j >> 2) & 3);
-                const uint32_t offj = (uint32_t)__shfl((int)off16, j, 64);
-                if (wbase + (uint32_t)j < a.n)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(fr + ((size_t)offj << 4) +
-                                                                        16 * c),
-                        (__attribute__((address_space(3))) void*)&s_win[wave][64 * k], 16, 0, 0);
-            }
-            uint4 c4 = make_uint4(0, 0, 0, 0);
-            if (live && len > 64u) c4 = reinterpret_cast<const uint4*>(p)[4];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                uint4 v = s_win[wave][4 * lane + (c ^ ((lane >> 2) & 3))];
-                if (!live || (c == 3 && len <= 48u)) v = make_uint4(0, 0, 0, 0);
-                w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-            }
-            w[16] = c4.x; w[17] = c4.y; w[18] = c4.z; w[19] = c4.w;
-        }
-#else
         if (live) {
             const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
@@ -935,7 +896,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 }
             }
         }
-#endif
         {
             const uint32_t nt = tile + gridDim.x;
             dsc_next = 0;
