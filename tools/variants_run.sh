@@ -10,7 +10,7 @@ run() {  # label, then env assignments for the variant
 }
 run default UPE_BENCH_EVENTS=1
 run noev UPE_BENCH_EVENTS=0
-if [ $# -eq 0 ]; then
+if [ $# -eq 0 ] && [ -z "${VARIANTS_NONE:-}" ]; then
   set -- a2=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a2.so \
          a4=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a4.so \
          a15=UPE_GPU_LIB_DIAG=$PWD/build/ablate/libupe_gpu_a15.so \

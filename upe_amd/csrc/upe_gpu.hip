@@ -77,7 +77,10 @@ constexpr int kTile = kBlock;
 constexpr int kWavesPerSimd = UPE_WAVES_PER_SIMD;   // 8 -> VGPR budget 64
 constexpr int kUnroll = 4;             // rules per early-exit check (rule table padding unit)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kLdsStatsMax = 4096;     // rule_stats histogrammed in LDS up to this many rules
+#ifndef UPE_LDS_STATS_MAX
+#define UPE_LDS_STATS_MAX 4096
+#endif
+constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr uint32_t kArpLdsSlots = 1024;   // ARP indexes up to 16 KB are staged in LDS
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
@@ -1060,11 +1063,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
 
         // ---- rule_stats: LDS histogram (same-address lanes serialise in the LDS atomic unit,
-        // cheaper than a cross-lane reduction per distinct rule) ----
-        if (lds_stats && !(kAblate & 4) && ok && ri != kNone) {
-            atomicAdd(&lds_hist[2 * ri], 1u);
-            atomicAdd(&lds_hist[2 * ri + 1], len);
-        }
+        // cheaper than a cross-lane reduction per distinct rule).  One 64-bit atomic per packet:
+        // the bin's low word counts packets, the high word bytes; neither carries into the other
+        // (a workgroup's packets and bytes each fit 32 bits, as the u32 views below assume) ----
+        if (lds_stats && !(kAblate & 4) && ok && ri != kNone)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&lds_hist[2 * ri]),
+                      ((unsigned long long)len << 32) | 1ull);
 
         // ---- per-lane totals and L1 bookkeeping ----
         c01 += (ok ? 1u : 0u) + (ok && ri != kNone ? 0x10000u : 0u);
@@ -1228,22 +1232,25 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // batch's verdict words by matched rule.  Workgroup (x, y) counts the packets of chunk x whose
 // rule falls in range y in LDS, then adds its nonzero bins to the per-sorted-index totals with
 // contiguous device atomics (credited to rule_id on the host, like small tables).  u32 bins
-// cannot overflow: a chunk holds at most 65536 packets of at most 65535 bytes.
+// cannot overflow: a chunk holds at most 65536 packets of at most 65535 bytes.  The host sizes
+// range (LDS bins) and chunk so that the grid fills the chip.
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t kHistRange = 8192;    // rules per workgroup: 64 KB of LDS
-constexpr uint32_t kHistChunk = 65536;   // packets per workgroup
+constexpr uint32_t kHistRange = 8192;    // most rules per workgroup: 64 KB of LDS
+constexpr uint32_t kHistChunk = 65536;   // most packets per workgroup
+constexpr uint32_t kHistChunkMin = 4096;
 
 __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint64_t* desc,
                                                      uint32_t n, uint32_t nrules,
-                                                     unsigned long long* stats_idx) {
+                                                     unsigned long long* stats_idx,
+                                                     uint32_t chunk, uint32_t range) {
     // one 64-bit bin per rule: packets << 32 | bytes (a chunk holds at most 65536 packets of
     // at most 65535 bytes, so neither half overflows)
-    __shared__ unsigned long long h[kHistRange];
-    const uint32_t r0 = blockIdx.y * kHistRange;
-    const uint32_t p0 = blockIdx.x * kHistChunk;
-    for (uint32_t k = threadIdx.x; k < kHistRange; k += 256) h[k] = 0;
+    extern __shared__ unsigned long long h[];   // [range]
+    const uint32_t r0 = blockIdx.y * range;
+    const uint32_t p0 = blockIdx.x * chunk;
+    for (uint32_t k = threadIdx.x; k < range; k += 256) h[k] = 0;
     __syncthreads();
-    const uint32_t pend = n - p0 < kHistChunk ? n : p0 + kHistChunk;
+    const uint32_t pend = n - p0 < chunk ? n : p0 + chunk;
     // four verdict words per thread per round, loaded together
     for (uint32_t i = p0 + 4 * threadIdx.x; i < pend; i += 4 * 256) {
         uint32_t v[4];
@@ -1259,7 +1266,7 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
-            in[j] = rb != 0 && rb - 1u - r0 < kHistRange;
+            in[j] = rb != 0 && rb - 1u - r0 < range;
             len[j] = in[j] ? (uint32_t)(desc[i + j] & 0xFFFFu) : 0u;
         }
 #pragma unroll
@@ -1267,7 +1274,7 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
             if (in[j]) atomicAdd(&h[(v[j] >> 8) - 1u - r0], (1ull << 32) | len[j]);
     }
     __syncthreads();
-    const uint32_t rend = nrules - r0 < kHistRange ? nrules : r0 + kHistRange;
+    const uint32_t rend = nrules - r0 < range ? nrules : r0 + range;
     for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
         const unsigned long long b = h[k >> 1];
         const unsigned long long x = (k & 1) ? (b & 0xFFFFFFFFull) : (b >> 32);
@@ -2147,10 +2154,16 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
         hipLaunchKernelGGL(upe_classify<false>, dim3(grid), dim3(kBlock), lds, s, a);
     HIP_TRY(hipGetLastError());
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
-        const dim3 hg((uint32_t)((n + kHistChunk - 1) / kHistChunk),
-                      (c->nrules_pad + kHistRange - 1) / kHistRange);
-        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), 0, s, d_verdict, d_desc, (uint32_t)n,
-                           c->nrules_pad, c->stats_idx);
+        // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
+        // kHistChunkMin) until the grid has about 2048 workgroups
+        const uint32_t range = c->nrules_pad < kHistRange ? c->nrules_pad : kHistRange;
+        const uint32_t nr = (c->nrules_pad + range - 1) / range;
+        uint32_t chunk = kHistChunk;
+        while (chunk > kHistChunkMin && ((n + chunk - 1) / chunk) * nr < 2048) chunk >>= 1;
+        const dim3 hg((uint32_t)((n + chunk - 1) / chunk), nr);
+        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), range * sizeof(unsigned long long), s,
+                           d_verdict, d_desc, (uint32_t)n, c->nrules_pad, c->stats_idx, chunk,
+                           range);
         HIP_TRY(hipGetLastError());
     }
     if (c->t_left && --c->t_left == 0) {
