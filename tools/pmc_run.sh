@@ -5,7 +5,7 @@
 set -e
 cfg=${1:-B}; shift || true
 groups=${*:-fetch write sq clk}
-steps="--steps 20 --warmup 2 --no-cpu-baseline --host-reps 0 --config $cfg"
+steps="--steps 20 --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg"
 for g in $groups; do
   case $g in
     fetch) ctr="FETCH_SIZE" ;;
