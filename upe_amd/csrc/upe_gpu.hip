@@ -1245,7 +1245,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // cannot overflow: a chunk holds at most 65536 packets of at most 65535 bytes.  The host sizes
 // range (LDS bins) and chunk so that the grid fills the chip.
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t kHistRange = 8192;    // most rules per workgroup: 64 KB of LDS
+#ifndef UPE_HIST_RANGE
+#define UPE_HIST_RANGE 8192
+#endif
+constexpr uint32_t kHistRange = UPE_HIST_RANGE;   // most rules per workgroup: 64 KB of LDS
 constexpr uint32_t kHistChunk = 65536;   // most packets per workgroup
 constexpr uint32_t kHistChunkMin = 4096;
 
