@@ -35,6 +35,8 @@ EVENT_EVERY = 20  # open a kernel-timing sample on every 20th timed step (10 sam
 EVENT_SPAN = 5    # each sample's HIP event pair brackets 5 consecutive launches
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
 WORKLOADS = {
+    "A": "A: 10k x 64B UDP/IPv4 pcap-replay records, rules.example (configs[0], the reference's "
+         "own CPU case), replayed as device-resident batches",
     "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",
     "C": "C: 1M IMIX 64/570/1518 v4+v6, 1k 5-tuple rules, ARP+NDP L3 fwd (configs[2])",
     "D": "D: 16M mixed/malformed, 64k rules (configs[3])",
@@ -221,8 +223,9 @@ def main() -> None:
     from upe_amd import gpu, shard, synth
 
     # this rank's static shard: a full batch of the configuration, its own seed
-    make = {"B": synth.config_b, "C": synth.config_c, "D": synth.config_d}[args.config]
-    kw = {"seed": {"B": 2, "C": 3, "D": 4}[args.config] + 1000 * rank}
+    make = {"A": synth.config_a, "B": synth.config_b, "C": synth.config_c,
+            "D": synth.config_d}[args.config]
+    kw = {"seed": {"A": 1, "B": 2, "C": 3, "D": 4}[args.config] + 1000 * rank}
     if args.packets:
         kw["n"] = args.packets
     wl = make(**kw)
@@ -373,7 +376,8 @@ def main() -> None:
                         f"{hr['reps']} passes, all ranks at once",
             }
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
-            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
+            # config A is the reference's one-worker pcap replay: time it on one core
+            out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads)
         print(json.dumps(out), flush=True)
     worker.close()
     if dist:

@@ -1,0 +1,3 @@
+bash tools/gpu_session.sh \
+ "A:200:python bench.py --config A" \
+ "hostA:200:python bench.py --config A --host-reps 10 --no-cpu-baseline --no-hbm-probe"
