@@ -1,0 +1,4 @@
+bash tools/gpu_session.sh \
+ "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+ "pmcD:300:bash tools/pmc_run.sh D fetch write" \
+ "profD:400:rocprofv3 --kernel-trace --stats -d gpurun_out/profD -o p --output-format csv -- python bench.py --config D --no-cpu-baseline"

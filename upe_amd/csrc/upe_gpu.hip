@@ -214,6 +214,8 @@ struct Args {
     const TssGroup* tg6;
     const uint4* tt4;
     const uint4* tt6;
+    const uint16_t* tf4;           // per slot: 16-bit fingerprint of its key, 0 = empty
+    const uint16_t* tf6;
     uint32_t ng4, ng6, tss;
     // the context's arrays, passed by value so that no kernel waits on a pointer load
     TilePay* pay;                    // [grid]
@@ -427,6 +429,11 @@ __host__ __device__ __forceinline__ uint32_t tss_hash(const uint32_t* k, int nw,
     h ^= h >> 16;
     return h;
 }
+// A slot's 16-bit fingerprint (never 0, which marks an empty slot).  The slot positions come
+// from the high bits of products of the hash, the tag from its low bits.
+__host__ __device__ __forceinline__ uint16_t tss_tag(uint32_t h) {
+    return (uint16_t)((h & 0xFFFFu) | 1u);
+}
 
 // First match through the tuple-space index for one packet family (F = 4 or 6).  Groups are
 // visited in order of their smallest sorted index, so once a lane's best index is below the
@@ -460,29 +467,40 @@ __device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32
             const uint32_t h = tss_hash(kw, nw, q[12]);
             const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
             const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
+            // fingerprints first (a few hundred KB, L2-resident): a slot is loaded only when
+            // its fingerprint matches, and then compared in full
+            const uint16_t* FP = F == 4 ? a.tf4 : a.tf6;
+            const uint32_t tag = tss_tag(h);
+            const bool m1 = FP[t1] == tag, m2 = FP[t2] == tag;
             uint32_t idx = kNone;
-            if constexpr (F == 4) {
-                const uint4 a1 = T[2 * t1], b1 = T[2 * t1 + 1];
-                const uint4 a2 = T[2 * t2], b2 = T[2 * t2 + 1];
-                const bool h1 = b1.y && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
-                                a1.w == kw[3];
-                const bool h2 = b2.y && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
-                                a2.w == kw[3];
-                idx = h1 ? b1.x : h2 ? b2.x : kNone;
-                const uint32_t ac = h1 ? b1.z : b2.z;
-                if (idx < best) act = ac << 16;
-            } else {
-                const uint4 a1 = T[3 * t1], b1 = T[3 * t1 + 1], c1 = T[3 * t1 + 2];
-                const uint4 a2 = T[3 * t2], b2 = T[3 * t2 + 1], c2 = T[3 * t2 + 2];
-                const bool h1 = (c1.w & 1u) && a1.x == kw[0] && a1.y == kw[1] && a1.z == kw[2] &&
-                                a1.w == kw[3] && b1.x == kw[4] && b1.y == kw[5] &&
-                                b1.z == kw[6] && b1.w == kw[7] && c1.x == kw[8] && c1.y == kw[9];
-                const bool h2 = (c2.w & 1u) && a2.x == kw[0] && a2.y == kw[1] && a2.z == kw[2] &&
-                                a2.w == kw[3] && b2.x == kw[4] && b2.y == kw[5] &&
-                                b2.z == kw[6] && b2.w == kw[7] && c2.x == kw[8] && c2.y == kw[9];
-                idx = h1 ? c1.z : h2 ? c2.z : kNone;
-                const uint32_t ac = (h1 ? c1.w : c2.w) >> 8;
-                if (idx < best) act = ac << 16;
+            if (m1 || m2) {
+                if constexpr (F == 4) {
+                    uint4 a1 = make_uint4(0, 0, 0, 0), b1 = a1, a2 = a1, b2 = a1;
+                    if (m1) { a1 = T[2 * t1]; b1 = T[2 * t1 + 1]; }
+                    if (m2) { a2 = T[2 * t2]; b2 = T[2 * t2 + 1]; }
+                    const bool h1 = m1 && b1.y && a1.x == kw[0] && a1.y == kw[1] &&
+                                    a1.z == kw[2] && a1.w == kw[3];
+                    const bool h2 = m2 && b2.y && a2.x == kw[0] && a2.y == kw[1] &&
+                                    a2.z == kw[2] && a2.w == kw[3];
+                    idx = h1 ? b1.x : h2 ? b2.x : kNone;
+                    const uint32_t ac = h1 ? b1.z : b2.z;
+                    if (idx < best) act = ac << 16;
+                } else {
+                    uint4 a1 = make_uint4(0, 0, 0, 0), b1 = a1, c1 = a1, a2 = a1, b2 = a1, c2 = a1;
+                    if (m1) { a1 = T[3 * t1]; b1 = T[3 * t1 + 1]; c1 = T[3 * t1 + 2]; }
+                    if (m2) { a2 = T[3 * t2]; b2 = T[3 * t2 + 1]; c2 = T[3 * t2 + 2]; }
+                    const bool h1 = m1 && (c1.w & 1u) && a1.x == kw[0] && a1.y == kw[1] &&
+                                    a1.z == kw[2] && a1.w == kw[3] && b1.x == kw[4] &&
+                                    b1.y == kw[5] && b1.z == kw[6] && b1.w == kw[7] &&
+                                    c1.x == kw[8] && c1.y == kw[9];
+                    const bool h2 = m2 && (c2.w & 1u) && a2.x == kw[0] && a2.y == kw[1] &&
+                                    a2.z == kw[2] && a2.w == kw[3] && b2.x == kw[4] &&
+                                    b2.y == kw[5] && b2.z == kw[6] && b2.w == kw[7] &&
+                                    c2.x == kw[8] && c2.y == kw[9];
+                    idx = h1 ? c1.z : h2 ? c2.z : kNone;
+                    const uint32_t ac = (h1 ? c1.w : c2.w) >> 8;
+                    if (idx < best) act = ac << 16;
+                }
             }
             best = min(best, idx);
         }
@@ -1435,6 +1453,8 @@ struct upe_gpu_ctx {
     TssGroup* tg6 = nullptr;
     uint4* tt4 = nullptr;
     uint4* tt6 = nullptr;
+    uint16_t* tf4 = nullptr;
+    uint16_t* tf6 = nullptr;
     uint32_t ng4 = 0, ng6 = 0;
     bool tss = false;
     uint32_t* compact_counts = nullptr;   // upe_gpu_compact: per-block counts
@@ -1689,7 +1709,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->compact_counts,
+                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1744,6 +1764,7 @@ namespace {
 struct TssFamily {
     std::vector<TssGroup> groups;
     std::vector<uint4> slots;
+    std::vector<uint16_t> fp;   // one per slot
 };
 
 bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
@@ -1817,9 +1838,12 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
         out.groups.push_back(d);
         const size_t base = out.slots.size();
         out.slots.resize(base + slot.size() * per, make_uint4(0, 0, 0, 0));
+        const size_t fbase = out.fp.size();
+        out.fp.resize(fbase + slot.size(), 0);
         for (size_t t = 0; t < slot.size(); ++t) {
             if (slot[t] < 0) continue;
             const Key& k = keys[slot[t]];
+            out.fp[fbase + t] = tss_tag(tss_hash(k.data(), nw, seed));
             uint4* e = &out.slots[base + t * per];
             const uint32_t act = act_code(rules[idx[slot[t]]].action.type);
             if (F == 4) {
@@ -1848,6 +1872,9 @@ int upload(TssGroup*& dst, const std::vector<TssGroup>& v) {
 }
 int upload(uint4*& dst, const std::vector<uint4>& v) {
     return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint4));
+}
+int upload(uint16_t*& dst, const std::vector<uint16_t>& v) {
+    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint16_t));
 }
 }  // namespace
 extern "C" {
@@ -1936,7 +1963,8 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             const size_t ng = f4.groups.size() + f6.groups.size();
             if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
                 if (upload(c->tg4, f4.groups) || upload(c->tg6, f6.groups) ||
-                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots))
+                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots) ||
+                    upload(c->tf4, f4.fp) || upload(c->tf6, f6.fp))
                     return -1;
                 c->ng4 = (uint32_t)f4.groups.size();
                 c->ng6 = (uint32_t)f6.groups.size();
@@ -2134,6 +2162,8 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
     a.tg6 = c->tg6;
     a.tt4 = c->tt4;
     a.tt6 = c->tt6;
+    a.tf4 = c->tf4;
+    a.tf6 = c->tf6;
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
     a.tss = c->tss ? 1u : 0u;
