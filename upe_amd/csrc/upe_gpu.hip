@@ -1259,23 +1259,28 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // rule_stats of large tables (more rules than an LDS histogram holds): a group-by of the
 // batch's verdict words by matched rule.  Workgroup (x, y) counts the packets of chunk x whose
 // rule falls in range y in LDS, then adds its nonzero bins to the per-sorted-index totals with
-// contiguous device atomics (credited to rule_id on the host, like small tables).  u32 bins
-// cannot overflow: a chunk holds at most 65536 packets of at most 65535 bytes.  The host sizes
-// range (LDS bins) and chunk so that the grid fills the chip.
+// contiguous device atomics (credited to rule_id on the host, like small tables).  The device
+// atomics dominate when a chunk sees each rule about once (config D: 64k rules), so chunks are
+// as large as about kHistTarget workgroups allow (fewer, longer workgroups measured slower) and
+// a bin packs packets << 40 |
+// bytes, which cannot overflow: a chunk holds at most 2^24 packets of at most 65535 bytes.
 // ------------------------------------------------------------------------------------------
 #ifndef UPE_HIST_RANGE
 #define UPE_HIST_RANGE 8192
 #endif
 constexpr uint32_t kHistRange = UPE_HIST_RANGE;   // most rules per workgroup: 64 KB of LDS
-constexpr uint32_t kHistChunk = 65536;   // most packets per workgroup
+constexpr uint32_t kHistChunk = 1u << 24;   // most packets per workgroup
 constexpr uint32_t kHistChunkMin = 4096;
+#ifndef UPE_HIST_TARGET
+#define UPE_HIST_TARGET 2048
+#endif
+constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
 
 __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint64_t* desc,
                                                      uint32_t n, uint32_t nrules,
                                                      unsigned long long* stats_idx,
                                                      uint32_t chunk, uint32_t range) {
-    // one 64-bit bin per rule: packets << 32 | bytes (a chunk holds at most 65536 packets of
-    // at most 65535 bytes, so neither half overflows)
+    // one 64-bit bin per rule: packets << 40 | bytes
     extern __shared__ unsigned long long h[];   // [range]
     const uint32_t r0 = blockIdx.y * range;
     const uint32_t p0 = blockIdx.x * chunk;
@@ -1302,13 +1307,13 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (in[j]) atomicAdd(&h[(v[j] >> 8) - 1u - r0], (1ull << 32) | len[j]);
+            if (in[j]) atomicAdd(&h[(v[j] >> 8) - 1u - r0], (1ull << 40) | len[j]);
     }
     __syncthreads();
     const uint32_t rend = nrules - r0 < range ? nrules : r0 + range;
     for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
         const unsigned long long b = h[k >> 1];
-        const unsigned long long x = (k & 1) ? (b & 0xFFFFFFFFull) : (b >> 32);
+        const unsigned long long x = (k & 1) ? (b & ((1ull << 40) - 1)) : (b >> 40);
         if (x) atomicAdd(&stats_idx[2 * (size_t)r0 + k], x);
     }
 }
@@ -2198,11 +2203,12 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
     HIP_TRY(hipGetLastError());
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
-        // kHistChunkMin) until the grid has about 2048 workgroups
+        // kHistChunkMin) while the grid has fewer than about kHistTarget workgroups
         const uint32_t range = c->nrules_pad < kHistRange ? c->nrules_pad : kHistRange;
         const uint32_t nr = (c->nrules_pad + range - 1) / range;
         uint32_t chunk = kHistChunk;
-        while (chunk > kHistChunkMin && ((n + chunk - 1) / chunk) * nr < 2048) chunk >>= 1;
+        while (chunk > kHistChunkMin && ((n + chunk / 2 - 1) / (chunk / 2)) * nr <= kHistTarget)
+            chunk >>= 1;
         const dim3 hg((uint32_t)((n + chunk - 1) / chunk), nr);
         hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), range * sizeof(unsigned long long), s,
                            d_verdict, d_desc, (uint32_t)n, c->nrules_pad, c->stats_idx, chunk,
