@@ -1261,9 +1261,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // rule falls in range y in LDS, then adds its nonzero bins to the per-sorted-index totals with
 // contiguous device atomics (credited to rule_id on the host, like small tables).  The device
 // atomics dominate when a chunk sees each rule about once (config D: 64k rules), so chunks are
-// as large as about kHistTarget workgroups allow (fewer, longer workgroups measured slower) and
-// a bin packs packets << 40 |
-// bytes, which cannot overflow: a chunk holds at most 2^24 packets of at most 65535 bytes.
+// as large as about kHistTarget workgroups allow (fewer, longer workgroups measured slower),
+// and a bin packs packets << 40 | bytes, which cannot overflow: a chunk holds at most 2^24
+// packets of at most 65535 bytes.
 // ------------------------------------------------------------------------------------------
 #ifndef UPE_HIST_RANGE
 #define UPE_HIST_RANGE 8192
