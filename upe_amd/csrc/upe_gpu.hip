@@ -81,6 +81,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #define UPE_LDS_STATS_MAX 4096
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
+constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
 constexpr uint32_t kArpLdsSlots = 1024;   // ARP indexes up to 16 KB are staged in LDS
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
@@ -170,7 +171,7 @@ struct DevState {
     TilePay* pay;                    // [grid]
     uint32_t* cand_tile;             // [ntiles], zero between batches
     unsigned long long* stats;       // [cap][2] worker rule_stats (mid-size and large tables)
-    unsigned long long* stats_idx;   // [nrules_pad][2] totals per sorted index (small tables)
+    unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2] totals per sorted index
 };
 
 // Neighbour index (built by upe_gpu_load_neigh): the entries a reference probe reaches, placed
@@ -221,7 +222,7 @@ struct Args {
     TilePay* pay;                    // [grid]
     uint32_t* cand_tile;             // [ntiles]
     unsigned long long* stats;       // [cap][2]
-    unsigned long long* stats_idx;   // [nrules_pad][2]
+    unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
 };
@@ -1168,14 +1169,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     STAMP(10);
 
-    // ---- rule_stats of mid-size tables: straight into the worker totals (the host reads them
-    // after the batch; nothing in this launch does) ----
+    // ---- rule_stats of mid-size tables: into one of kStatReps replicas of the per-sorted-index
+    // totals (the host sums them and credits rule_id; nothing in this launch reads them), so
+    // that the hot rules' counters take 1/kStatReps of the workgroups' atomics each ----
     if (lds_stats && !small_stats && !(kAblate & 4)) {
+        unsigned long long* rep = a.stats_idx + (size_t)(blockIdx.x % kStatReps) * 2 * a.nrules_pad;
         for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) {
             const uint32_t v = lds_hist[k];
-            if (v)
-                atomicAdd(&a.stats[2 * (uint32_t)a.rinfo[k >> 1].y + (k & 1)],
-                          (unsigned long long)v);
+            if (v) atomicAdd(&rep[k], (unsigned long long)v);
         }
     }
     if (wave == 0) {
@@ -1314,7 +1315,7 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
     for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
         const unsigned long long b = h[k >> 1];
         const unsigned long long x = (k & 1) ? (b & ((1ull << 40) - 1)) : (b >> 40);
-        if (x) atomicAdd(&stats_idx[2 * (size_t)r0 + k], x);
+        if (x) atomicAdd(&stats_idx[(size_t)(blockIdx.x % kStatReps) * 2 * nrules + 2 * (size_t)r0 + k], x);
     }
 }
 
@@ -1735,18 +1736,26 @@ namespace {
 // Credit the sorted-index totals of the current table to rule_stats[rule_id] (device) and clear
 // them: called before the table changes, so a reload keeps every count (src/main.c:216-282
 // swaps rule_stats with the table; here the counts simply carry over by rule_id).
-// Tables whose counts are kept per sorted index (credited to rule_id on the host): small ones
-// (replicated accumulators) and large ones (upe_rule_hist); mid-size ones go straight to rule_id.
-bool idx_stats(const upe_gpu_ctx* c) {
-    return c->nrules_pad <= (uint32_t)kSmallRules || c->nrules_pad > (uint32_t)kLdsStatsMax;
+// Every table size keeps its counts per sorted index, in kStatReps replicas: small tables (the
+// last workgroup adds the folded accumulators to replica 0), mid-size ones (each workgroup's LDS
+// bins) and large ones (upe_rule_hist).  The host sums the replicas and credits rule_id.
+int read_stats_idx(upe_gpu_ctx* c, std::vector<unsigned long long>& idx) {
+    const size_t E = 2 * (size_t)c->nrules_pad;
+    std::vector<unsigned long long> all(E * kStatReps);
+    HIP_TRY(hipMemcpy(all.data(), c->stats_idx, all.size() * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost));
+    idx.assign(E, 0);
+    for (size_t r = 0; r < (size_t)kStatReps; ++r)
+        for (size_t e = 0; e < E; ++e) idx[e] += all[r * E + e];
+    return 0;
 }
 
 int fold_stats_idx(upe_gpu_ctx* c) {
-    if (!c->stats_idx || c->rinfo_host.empty() || !idx_stats(c)) return 0;
+    if (!c->stats_idx || c->rinfo_host.empty()) return 0;
     const size_t E = 2 * (size_t)c->nrules_pad;
-    std::vector<unsigned long long> idx(E), st(2 * c->cap);
+    std::vector<unsigned long long> idx, st(2 * c->cap);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(idx.data(), c->stats_idx, E * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (read_stats_idx(c, idx) != 0) return -1;
     bool any = false;
     for (unsigned long long v : idx) any |= v != 0;
     if (!any) return 0;
@@ -1756,7 +1765,7 @@ int fold_stats_idx(upe_gpu_ctx* c) {
         if (idx[e]) st[2 * (size_t)(uint32_t)c->rinfo_host[e >> 1].y + (e & 1)] += idx[e];
     HIP_TRY(hipMemcpy(c->stats, st.data(), st.size() * sizeof(unsigned long long),
                       hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(c->stats_idx, 0, E * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(c->stats_idx, 0, E * kStatReps * sizeof(unsigned long long)));
     return 0;
 }
 }  // namespace
@@ -1944,8 +1953,8 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         HIP_TRY(hipMalloc(&c->rinfo, pad * sizeof(int2)));
         if (c->stats_idx) (void)hipFree(c->stats_idx);
         c->stats_idx = nullptr;
-        HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * kStatReps * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * kStatReps * sizeof(unsigned long long)));
         c->rules_alloc = pad;
         if (publish(c) != 0) return -1;
     }
@@ -2577,12 +2586,11 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
     if (rule_stats) {
         const size_t k = capacity < c->cap ? capacity : c->cap;
         HIP_TRY(hipMemcpy(rule_stats, c->stats, k * sizeof(upe_rule_stat_t), hipMemcpyDeviceToHost));
-        if (idx_stats(c) && c->stats_idx) {
-            // small tables keep this table's counts per sorted index: credit them to rule_id
+        if (c->stats_idx && !c->rinfo_host.empty()) {
+            // this table's counts are kept per sorted index: credit them to rule_id
             const size_t E = 2 * (size_t)c->nrules_pad;
-            std::vector<unsigned long long> idx(E);
-            HIP_TRY(hipMemcpy(idx.data(), c->stats_idx, E * sizeof(unsigned long long),
-                              hipMemcpyDeviceToHost));
+            std::vector<unsigned long long> idx;
+            if (read_stats_idx(c, idx) != 0) return -1;
             for (size_t e = 0; e < E; ++e) {
                 const uint32_t rid = (uint32_t)c->rinfo_host[e >> 1].y;
                 if (!idx[e] || rid >= k) continue;
@@ -2600,7 +2608,8 @@ int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
     HIP_TRY(hipMemsetAsync(c->totals, 0, sizeof(DevTotals), c->stream));
     HIP_TRY(hipMemsetAsync(c->stats, 0, c->cap * 2 * sizeof(unsigned long long), c->stream));
     if (c->stats_idx)
-        HIP_TRY(hipMemsetAsync(c->stats_idx, 0, (size_t)c->rules_alloc * 2 * sizeof(unsigned long long),
+        HIP_TRY(hipMemsetAsync(c->stats_idx, 0,
+                               (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long),
                                c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->have_batch = false;
