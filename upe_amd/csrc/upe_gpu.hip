@@ -521,21 +521,16 @@ struct Parsed {
     uint32_t ttl, c1w1, c1w2;      // TTL / hop, and bytes 20..27 as they are forwarded
 };
 
-// Inlined (only waves holding such a packet run it): as an out-of-line call it made every
-// call site save the caller's live registers to scratch, ~100 bytes of private-memory traffic
-// per slow packet (config D: 1.7 GB written per 16M batch; 2.32 -> 1.82 ms once inlined).
+// Two forms (only waves holding such a packet run either): inlined, and an out-of-line call.
+// The call saves the caller's live registers to scratch, ~100 bytes of private-memory traffic
+// per slow packet (config D: 1.7 GB written per 16M batch; 2.32 -> 1.82 ms inlined), but keeps
+// the fast path's register allocation lean (config B, which has no slow packets: 34.4 vs
+// 35.1 us inlined).  The tuple-space kernel, used for the large tables of the stress
+// configuration, inlines it; the scan kernel calls it.
 struct Port {
     uint32_t mac_lo, mac_hi, ip4;
 };
-#ifndef UPE_GP_INLINE
-#define UPE_GP_INLINE 1
-#endif
-#if UPE_GP_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r) {
+__device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r) {
     r.ok = false; r.consumed = false; r.v6 = false; r.flags = 0;
     r.proto = r.sport = r.dport = 0;
 #pragma unroll
@@ -665,6 +660,9 @@ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r) {
             // (len >= 54: only a fast-path packet; reached here when len < 54 -> parse fails)
         }
     }
+}
+__device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len, Parsed& r) {
+    general_path(a, p, len, r);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -983,7 +981,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const bool slow = live && !fast4 && !fast6;
         if (__any(slow) && slow) {
             Parsed g;
-            general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
+            if constexpr (kTssMode)
+                general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
+            else
+                general_path_call(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
             r = g;
         }
 
