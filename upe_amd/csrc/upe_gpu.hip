@@ -344,6 +344,35 @@ __device__ __forceinline__ bool ndp_lookup(const NeighIndex& x, const uint32_t i
     return h1 || h2;
 }
 
+// Both families in one lookup: the IPv4 (ARP) and IPv6 (NDP) lanes of a wave issue their slot
+// loads together, so a mixed wave waits for one memory round trip, not one per family.
+__device__ __forceinline__ bool neigh_lookup(const NeighIndex& arp, const NeighIndex& ndp,
+                                             bool v6, const uint32_t d[4], uint32_t& lo,
+                                             uint32_t& hi) {
+    const uint4* t = v6 ? ndp.t : arp.t;
+    const uint32_t bits = v6 ? ndp.bits : arp.bits;
+    const uint32_t seed = v6 ? ndp.seed : arp.seed;
+    if (bits == 0) return false;
+    const uint32_t k = v6 ? fold_v6(d) : d[0];
+    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits);
+    const uint32_t sh = v6 ? 1u : 0u;   // an NDP slot is two uint4: address, then MAC
+    const uint4 a1 = t[t1 << sh], a2 = t[t2 << sh];
+    uint4 m1 = a1, m2 = a2;
+    if (v6) {
+        m1 = t[2 * t1 + 1];
+        m2 = t[2 * t2 + 1];
+    }
+    const bool h1 = v6 ? (((m1.y >> 16) & 1u) && a1.x == d[0] && a1.y == d[1] && a1.z == d[2] &&
+                          a1.w == d[3])
+                       : (((a1.z >> 16) & 1u) && a1.x == d[0]);
+    const bool h2 = v6 ? (((m2.y >> 16) & 1u) && a2.x == d[0] && a2.y == d[1] && a2.z == d[2] &&
+                          a2.w == d[3])
+                       : (((a2.z >> 16) & 1u) && a2.x == d[0]);
+    lo = h1 ? (v6 ? m1.x : a1.y) : (v6 ? m2.x : a2.y);
+    hi = (h1 ? (v6 ? m1.y : a1.z) : (v6 ? m2.y : a2.z)) & 0xFFFFu;
+    return h1 || h2;
+}
+
 // Does each L1 entry agree with the table?  (ARP: an entry for 0.0.0.0 is never consulted,
 // src/worker.c:186, so it always "agrees".)
 __device__ void refresh_ok(DevL1* l1, const NeighIndex& arp, const NeighIndex& ndp) {
@@ -996,11 +1025,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint32_t mlo = 0, mhi = 0;
         bool nhit = false;
         if (ok && r.ttl > 1u && !(kAblate & 2)) {
-            if (!r.v6)
-                nhit = a.arp_lds ? arp_lookup_lds(s_arp, a.arp.bits, a.arp.seed, r.d[0], mlo, mhi)
-                                 : arp_lookup(a.arp, r.d[0], mlo, mhi);
+            if (!r.v6 && a.arp_lds)
+                nhit = arp_lookup_lds(s_arp, a.arp.bits, a.arp.seed, r.d[0], mlo, mhi);
             else
-                nhit = ndp_lookup(a.ndp, r.d, mlo, mhi);
+                nhit = neigh_lookup(a.arp, a.ndp, r.v6, r.d, mlo, mhi);
         }
 
         // ---- rule_table_match ----
