@@ -1,19 +1,22 @@
 """bench.py — device-resident Mpps of the UPE worker hot path on MI355X (BASELINE.json metric).
 
-A "step" is one pass of the hot path (classify + finalize through the C ABI upe_gpu_process)
-over one batch already resident in HBM.  At N=1 the workload is BASELINE.json configs[1]
-(config B: 1M x 64 B UDP/IPv4, 8 rules).  Every step gets its own pristine copy of the batch
-(the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the work),
-which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
+A "step" is one pass of the hot path (one upe_gpu_process call through the C ABI: the classify
+launch, plus the rule_stats group-by for tables over 4096 rules) over one batch already resident
+in HBM.  At N=1 the workload is BASELINE.json configs[1] (config B: 1M x 64 B UDP/IPv4, 8 rules);
+--config A / C / D run the other configurations.  Every step gets its own pristine copy of the
+batch (the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the
+work), which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
 per GPU, each with its own static shard of the packet stream (a full config-B batch per step,
 tables replicated), no data-path collective — weak scaling.  torch.distributed carries only the
 barrier and the max-over-ranks time.
 
-Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per classify launch
-(B(p) = 8 + E(p) + 4 + W(p)) / the classify kernel's mean duration, measured
-with HIP events on the launch stream over the timed region.  cpu_baseline = the reference
+Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch (SURVEY.md
+§8(d): B(p) = 8 + E(p) + 4 + W(p)) / the mean launch duration, measured with HIP events on the
+launch stream over the timed region (each sample's event pair brackets EVENT_SPAN consecutive
+launches); roofline.traffic = HBM bytes per launch from the committed PMC passes
+(profiles/pmc_config<X>.json).  cpu_baseline = the reference
 src/worker.c (oracle/_ref, built from the reference sources) timed on this host's cores over a
 bounded sample of the same workload.
 """
