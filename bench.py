@@ -81,6 +81,41 @@ def rule_evals(wl, verdict: np.ndarray) -> int:
     return int(np.where(rule > 0, rule, np.where(parsed, len(wl.rules), 0)).sum())
 
 
+def shared_gpu_workers(torch, dev, wl, worker0, pool, stride: int, copies: int, desc,
+                       workers: int, steps: int) -> dict:
+    """W worker contexts on one GPU (the reference runs several worker threads; each maps to a
+    context): worker w takes the batch copies k with k % W == w, on its own stream, so one
+    worker's per-launch start and tail overlap another's middle.  Outside the timed region of
+    `value`."""
+    from upe_amd import gpu
+
+    ws = [worker0] + [gpu.GpuWorker(dev.index, wl.capacity) for _ in range(workers - 1)]
+    for w in ws[1:]:
+        w.configure(wl)
+    streams = [torch.cuda.Stream(dev) for _ in ws]
+    verdicts = [torch.empty(wl.n, dtype=torch.int32, device=dev) for _ in ws]
+    base = pool.data_ptr()
+    mine = [[base + (k % copies) * stride for k in range(copies) if k % workers == j]
+            for j in range(workers)]
+
+    def run(count: int) -> None:
+        for j, w in enumerate(ws):
+            lst = [mine[j][k % len(mine[j])] for k in range(count)]
+            w.process_batches(lst, desc, verdicts[j], wl.n, streams[j].cuda_stream)
+
+    run(3)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    for w in ws[1:]:
+        w.close()
+    return {"workers": workers, "value": round(workers * steps * wl.n / dt / 1e6, 2),
+            "unit": "Mpps", "ms_per_round": round(dt / steps * 1e3, 5),
+            "what": f"{workers} worker contexts on this GPU, {steps} batches each, own streams"}
+
+
 def hbm_probe(torch, dev, gib: int = 4, reps: int = 10) -> dict:
     """Achievable HBM streaming rates on this GPU (SURVEY.md §8(d) asks for them beside the
     nominal 8 TB/s): a device-to-device copy and a read-only reduction over `gib` GiB buffers,
@@ -198,6 +233,10 @@ def main() -> None:
                          "rocprof summary of the default command holds only full-batch "
                          "launches; DESIGN.md quotes a --host-reps 10 run)")
     ap.add_argument("--host-chunk", type=int, default=0)
+    ap.add_argument("--workers-per-gpu", type=int, default=0,
+                    help="also time W worker contexts sharing this GPU, each on its own stream "
+                         "with its own batches and L1 state, as W reference worker threads would "
+                         "(reported beside value, never as value)")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the achievable-bandwidth probe (copy / read kernels)")
     args = ap.parse_args()
@@ -297,6 +336,10 @@ def main() -> None:
     v_first = verdict.cpu().numpy().view(np.uint32).copy()
     classify_ms, finalize_ms, launches = worker.timing_read()
     worker.timing_enable(False)
+    shared = None
+    if args.workers_per_gpu > 1:
+        shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
+                                    args.workers_per_gpu, args.steps)
     probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
@@ -365,6 +408,8 @@ def main() -> None:
                         "batches (src/rule_table.c:163-176) / wall time",
             },
         }
+        if shared:
+            out["workers_sharing_gpu"] = shared
         if hr:
             out["host_roundtrip"] = {
                 "value": round(hr["packets"] * world / hr["seconds"] / 1e6, 2), "unit": "Mpps",
