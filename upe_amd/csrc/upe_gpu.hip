@@ -82,7 +82,10 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
-constexpr uint32_t kArpLdsSlots = 1024;   // ARP indexes up to 16 KB are staged in LDS
+#ifndef UPE_ARP_LDS_SLOTS
+#define UPE_ARP_LDS_SLOTS 1024
+#endif
+constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;   // ARP indexes up to 16 KB are staged in LDS
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kShards = 8;             // arrival-ticket shards
