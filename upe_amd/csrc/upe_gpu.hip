@@ -227,6 +227,7 @@ struct Args {
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
+    uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
 };
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
@@ -1113,6 +1114,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
         if (live) a.verdict[i] = code | flags | rbits;
+        if (a.lens16 && live) a.lens16[i] = (uint16_t)len;   // 2 B/packet for upe_rule_hist
         if (a.flow_hash && live) {
             // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
             // key parse_flow_key gives the RX thread (src/rx_pcap.c:71-72), 0 if it fails
@@ -1308,9 +1310,10 @@ constexpr uint32_t kHistChunkMin = 4096;
 #endif
 constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
 
-__global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint64_t* desc,
+__global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint16_t* lens,
                                                      uint32_t n, uint32_t nrules,
                                                      unsigned long long* stats_idx,
+                                                     unsigned long long* stats_pk,
                                                      uint32_t chunk, uint32_t range) {
     // one 64-bit bin per rule: packets << 40 | bytes
     extern __shared__ unsigned long long h[];   // [range]
@@ -1329,13 +1332,23 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = i + j < pend ? verdict[i + j] : 0u;
         }
+        // the frame lengths the classify pass left, four to an 8-byte load (a quarter of the
+        // descriptor bytes: every range's workgroups read them again)
         uint32_t len[4];
         bool in[4];
+        bool any = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
             in[j] = rb != 0 && rb - 1u - r0 < range;
-            len[j] = in[j] ? (uint32_t)(desc[i + j] & 0xFFFFu) : 0u;
+            any |= in[j];
+        }
+        if (any && i + 4 <= pend && (i & 3) == 0) {
+            const uint2 q = *reinterpret_cast<const uint2*>(lens + i);
+            len[0] = q.x & 0xFFFFu; len[1] = q.x >> 16; len[2] = q.y & 0xFFFFu; len[3] = q.y >> 16;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) len[j] = in[j] ? (uint32_t)lens[i + j] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1343,10 +1356,34 @@ __global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, co
     }
     __syncthreads();
     const uint32_t rend = nrules - r0 < range ? nrules : r0 + range;
+    if (stats_pk) {
+        // one packed atomic per bin (the launch checked that a replica's packets fit 24 bits, so
+        // its bytes fit 40); upe_stats_unpack adds the packed words to stats_idx afterwards
+        unsigned long long* pk = stats_pk + (size_t)(blockIdx.x % kStatReps) * nrules + r0;
+        for (uint32_t k = threadIdx.x; k < rend - r0; k += 256) {
+            const unsigned long long b = h[k];
+            if (b) atomicAdd(&pk[k], b);
+        }
+        return;
+    }
     for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
         const unsigned long long b = h[k >> 1];
         const unsigned long long x = (k & 1) ? (b & ((1ull << 40) - 1)) : (b >> 40);
         if (x) atomicAdd(&stats_idx[(size_t)(blockIdx.x % kStatReps) * 2 * nrules + 2 * (size_t)r0 + k], x);
+    }
+}
+
+// The packed group-by totals of one batch into stats_idx ([kStatReps][nrules][2]), re-armed to
+// zero.  Each word has one thread, and nothing else touches either array until the next launch.
+__global__ void __launch_bounds__(256) upe_stats_unpack(unsigned long long* stats_pk,
+                                                        unsigned long long* stats_idx,
+                                                        uint32_t words) {
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < words; e += gridDim.x * 256) {
+        const unsigned long long b = stats_pk[e];
+        if (!b) continue;
+        stats_pk[e] = 0;
+        stats_idx[2 * (size_t)e] += b >> 40;
+        stats_idx[2 * (size_t)e + 1] += b & ((1ull << 40) - 1);
     }
 }
 
@@ -1484,6 +1521,9 @@ struct upe_gpu_ctx {
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
+    unsigned long long* stats_pk = nullptr;    // [kStatReps][rules_alloc] one batch, packed
+    uint16_t* lens16 = nullptr;                // [lens_alloc] frame lengths (group-by tables)
+    size_t lens_alloc = 0;
     std::vector<int2> rinfo_host;              // (action, rule_id) per sorted index
     // tuple-space index of large tables (null when the linear scan is used)
     TssGroup* tg4 = nullptr;
@@ -1745,7 +1785,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->arp, c->ndp, c->st, c->stats,
+    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->stats_pk, c->lens16, c->arp, c->ndp, c->st, c->stats,
                     c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens};
     for (void* b : bufs)
@@ -1983,9 +2023,13 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         HIP_TRY(hipMalloc(&c->rv6, pad * sizeof(RuleV6)));
         HIP_TRY(hipMalloc(&c->rinfo, pad * sizeof(int2)));
         if (c->stats_idx) (void)hipFree(c->stats_idx);
+        if (c->stats_pk) (void)hipFree(c->stats_pk);
         c->stats_idx = nullptr;
+        c->stats_pk = nullptr;
         HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * kStatReps * sizeof(unsigned long long)));
         HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * kStatReps * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc(&c->stats_pk, pad * kStatReps * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(c->stats_pk, 0, pad * kStatReps * sizeof(unsigned long long)));
         c->rules_alloc = pad;
         if (publish(c) != 0) return -1;
     }
@@ -2218,6 +2262,18 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
     a.stats_idx = c->stats_idx;
     a.flow_hash = d_flow_hash;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
+    a.lens16 = nullptr;
+    if (!lds_stats && n > 0 && !(kAblate & 4)) {
+        if (n > c->lens_alloc) {
+            if (c->lens16) (void)hipFree(c->lens16);
+            c->lens16 = nullptr;
+            c->lens_alloc = 0;
+            const size_t want = (n + n / 4 + 64) & ~(size_t)3;
+            HIP_TRY(hipMalloc(&c->lens16, want * sizeof(uint16_t)));
+            c->lens_alloc = want;
+        }
+        a.lens16 = c->lens16;
+    }
     const size_t hist = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
     // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
     // array 16-byte aligned after the bins)
@@ -2250,10 +2306,19 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
         while (chunk > kHistChunkMin && ((n + chunk / 2 - 1) / (chunk / 2)) * nr <= kHistTarget)
             chunk >>= 1;
         const dim3 hg((uint32_t)((n + chunk - 1) / chunk), nr);
+        // packed bins when no replica can collect 2^24 packets (nor so 2^40 bytes) in one batch
+        const uint64_t per_rep = (uint64_t)((hg.x + kStatReps - 1) / kStatReps) * chunk;
+        const bool packed = per_rep < (1ull << 24);
         hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), range * sizeof(unsigned long long), s,
-                           d_verdict, d_desc, (uint32_t)n, c->nrules_pad, c->stats_idx, chunk,
-                           range);
+                           d_verdict, c->lens16, (uint32_t)n, c->nrules_pad, c->stats_idx,
+                           packed ? c->stats_pk : nullptr, chunk, range);
         HIP_TRY(hipGetLastError());
+        if (packed) {
+            const uint32_t words = kStatReps * c->nrules_pad;
+            hipLaunchKernelGGL(upe_stats_unpack, dim3((words + 255) / 256), dim3(256), 0, s,
+                               c->stats_pk, c->stats_idx, words);
+            HIP_TRY(hipGetLastError());
+        }
     }
     if (c->t_left && --c->t_left == 0) {
         HIP_TRY(hipEventRecord(c->ev[c->ev_used + 1], s));
