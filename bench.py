@@ -1,8 +1,10 @@
 """bench.py — device-resident Mpps of the UPE worker hot path on MI355X (BASELINE.json metric).
 
-A "step" is one pass of the hot path (one upe_gpu_process call through the C ABI: the classify
-launch, plus the rule_stats group-by for tables over 4096 rules) over one batch already resident
-in HBM.  At N=1 the workload is BASELINE.json configs[1] (config B: 1M x 64 B UDP/IPv4, 8 rules);
+A "step" is one pass of the hot path (one upe_gpu_process_emit call through the C ABI: the
+classify launch, plus the rule_stats group-by for tables over 4096 rules) over one batch already
+resident in HBM.  The default output mode is emit (include/upe_gpu.h): verdicts plus one 16-byte
+rewritten-header record per packet, frames read only; --mode inplace rewrites the frames in place
+as upe_gpu_process does, and the JSON line carries the other mode's rate too ("other_mode").  At N=1 the workload is BASELINE.json configs[1] (config B: 1M x 64 B UDP/IPv4, 8 rules);
 --config A / C / D run the other configurations.  Every step gets its own pristine copy of the
 batch (the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the
 work), which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
@@ -46,8 +48,9 @@ WORKLOADS = {
 }
 
 
-def algorithmic_bytes(wl, verdict: np.ndarray) -> np.ndarray:
-    """B(p) per packet, SURVEY.md §8(d)."""
+def algorithmic_bytes(wl, verdict: np.ndarray, emit: bool = False) -> np.ndarray:
+    """B(p) per packet, SURVEY.md §8(d).  In emit mode W(p) is the 16-byte record of a forwarded
+    packet (the records of other packets are zero and not counted)."""
     from upe_amd.layout import desc_lens, desc_offsets
 
     offs = desc_offsets(wl.desc)
@@ -68,6 +71,8 @@ def algorithmic_bytes(wl, verdict: np.ndarray) -> np.ndarray:
     fwd = code == 4
     hit = (verdict & 0x10) != 0
     W = np.where(fwd & is4, 3, 0) + np.where(fwd & is6, 1, 0) + np.where(fwd & hit, 12, 0)
+    if emit:
+        W = np.where(fwd, 16, 0)
     return 8 + E + 4 + W
 
 
@@ -143,10 +148,11 @@ def hbm_probe(torch, dev, gib: int = 4, reps: int = 10) -> dict:
             "method": f"torch copy_ (read + write) and sum (read) over {gib} GiB, HIP events"}
 
 
-def pmc_traffic(config: str, packets: int):
+def pmc_traffic(config: str, packets: int, mode: str):
     """HBM bytes per classify launch from the committed PMC passes of this kernel
-    (profiles/pmc_config<X>.json, made by tools/pmc_run.sh + tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    (profiles/pmc_config<X>[_emit].json, made by tools/pmc_run.sh + tools/pmc_traffic.py), or
+    None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}{'_emit' if mode == 'emit' else ''}.json")
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
@@ -239,6 +245,11 @@ def main() -> None:
                          "(reported beside value, never as value)")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the achievable-bandwidth probe (copy / read kernels)")
+    ap.add_argument("--mode", default="emit", choices=["emit", "inplace"],
+                    help="emit: rewritten-header records, frames read only (upe_gpu_process_emit);"
+                         " inplace: frames rewritten in place (upe_gpu_process)")
+    ap.add_argument("--no-other-mode", action="store_true",
+                    help="skip timing the other output mode after the timed region")
     args = ap.parse_args()
 
     import torch
@@ -290,13 +301,17 @@ def main() -> None:
         pool[c * stride: c * stride + fbytes].copy_(pristine)
     desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=dev)
     base = pool.data_ptr()
     torch.cuda.synchronize(dev)
 
-    def steps(k0: int, count: int) -> None:
-        # queued from native code (upe_gpu_process_batches): no Python round trip per batch
-        worker.process_batches([base + (k % copies) * stride for k in range(k0, k0 + count)],
-                               desc, verdict, n, sh)
+    def steps(k0: int, count: int, mode: str = args.mode) -> None:
+        # queued from native code (upe_gpu_process_batches[_emit]): no Python round trip per batch
+        ptrs = [base + (k % copies) * stride for k in range(k0, k0 + count)]
+        if mode == "emit":
+            worker.process_batches_emit(ptrs, desc, verdict, hdr, n, sh)
+        else:
+            worker.process_batches(ptrs, desc, verdict, n, sh)
 
     steps(0, args.warmup)
     torch.cuda.synchronize(dev)
@@ -336,6 +351,24 @@ def main() -> None:
     v_first = verdict.cpu().numpy().view(np.uint32).copy()
     classify_ms, finalize_ms, launches = worker.timing_read()
     worker.timing_enable(False)
+    # the other output mode over the same number of steps (after the timed region; each step
+    # again on its own batch copy), so the line shows both: emit <-> in-place rewrite
+    other = None
+    if not args.no_other_mode:
+        om = "inplace" if args.mode == "emit" else "emit"
+        steps(0, min(args.warmup, 5), om)
+        worker.timing_span(EVENT_EVERY if events else 0, EVENT_SPAN)
+        torch.cuda.synchronize(dev)
+        ta = time.perf_counter()
+        steps(args.warmup, args.steps, om)
+        torch.cuda.synchronize(dev)
+        tb = time.perf_counter()
+        oc_ms, _, ol = worker.timing_read()
+        worker.timing_enable(False)
+        other = {"mode": om, "value": round(n * args.steps / (tb - ta) / 1e6, 2), "unit": "Mpps",
+                 "ms_per_step": round((tb - ta) / args.steps * 1e3, 5),
+                 "kernel_ms": round(oc_ms / ol, 5) if ol else None,
+                 "what": "this rank alone, same batches, timed after the main region"}
     shared = None
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
@@ -358,8 +391,8 @@ def main() -> None:
         hr["seconds"] = shard.max_over_ranks(hr["seconds"], dist, dev)
 
     if rank == 0:
-        bpp = algorithmic_bytes(wl, v_first)
-        traffic = pmc_traffic(args.config, n)
+        bpp = algorithmic_bytes(wl, v_first, emit=args.mode == "emit")
+        traffic = pmc_traffic(args.config, n, args.mode)
         bytes_per_launch = float(bpp.sum())
         kern_s = classify_ms / launches / 1e3 if launches else float("nan")
         achieved = bytes_per_launch / kern_s / 1e9
@@ -379,7 +412,11 @@ def main() -> None:
             "data": "synthetic (seeded upe_amd.synth, per-rank shard), resident in HBM",
             "config": {"workload": WORKLOADS[args.config], "packets_per_gpu_step": n,
                        "rules": int(len(wl.rules)), "parallelism": f"static shards x{world}, "
-                       "tables replicated, no RCCL on the data path"},
+                       "tables replicated, no RCCL on the data path",
+                       "output": ("emit: verdict + 16-B rewritten-header record per packet, "
+                                  "frames read only (upe_gpu_process_emit)")
+                       if args.mode == "emit" else
+                       "inplace: verdict per packet, frames rewritten in place (upe_gpu_process)"},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -387,8 +424,9 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "traffic_source": (f"profiles/pmc_config{args.config}.json (rocprofv3 PMC, "
-                                   "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
+                "traffic_source": (f"profiles/pmc_config{args.config}"
+                                   f"{'_emit' if args.mode == 'emit' else ''}.json (rocprofv3 "
+                                   "PMC, 2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
                 "kernel": "upe_classify",
                 "kernel_ms": round(kern_s * 1e3, 5),
                 "finalize_ms": round(finalize_ms / max(launches, 1), 5),
@@ -408,6 +446,8 @@ def main() -> None:
                         "batches (src/rule_table.c:163-176) / wall time",
             },
         }
+        if other:
+            out["other_mode"] = other
         if shared:
             out["workers_sharing_gpu"] = shared
         if hr:

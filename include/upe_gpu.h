@@ -218,6 +218,36 @@ int upe_gpu_get_l1(upe_gpu_ctx_t *ctx, upe_l1_state_t *l1);
 int upe_gpu_process(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                     uint32_t *d_verdict, size_t n, void *stream);
 
+/* Rewritten-header record (emit mode), 16 bytes per packet.  process_packet rewrites at most
+ * three places of a forwarded frame (src/worker.c:162-244): bytes 0..11 (dst MAC = the next-hop
+ * MAC and src MAC = tx->eth_addr on a neighbour hit), the TTL (IPv4 byte 22) with the header
+ * checksum (bytes 24..25), or the hop limit (IPv6 byte 21).  Emit mode leaves the frame alone
+ * and writes those bytes here instead, one coalesced 16-byte store per packet:
+ *   b[0..11]  bytes 0..11 of the forwarded frame (the original MACs when the lookup missed)
+ *   b[12]     new TTL (IPv4) or hop limit (IPv6)
+ *   b[13..14] new IPv4 header checksum as stored at frame bytes 24..25 (0 for IPv6)
+ *   b[15]     4 or 6: the packet was forwarded (verdict code UPE_V_FWD) as that family;
+ *             0 for every other verdict (the record is then all zero)
+ * upe_hdr_apply(frame, rec) turns a frame into exactly the bytes process_packet leaves in
+ * b->data; it does nothing when b[15] == 0. */
+typedef struct {
+    uint8_t b[16];
+} upe_hdr_rec_t;
+
+/* upe_gpu_process() in emit mode: d_hdr[i] (device, n records, 16-byte aligned) receives packet
+ * i's rewritten header bytes and the frames are not written — except the ARP requests answered
+ * in place (UPE_VF_ARP_REPLY), which the reference transmits at once (src/worker.c:40-52).
+ * Verdicts, counters, rule_stats and the L1 state are exactly those of upe_gpu_process().  This
+ * is the layout for a TX path that sends header and payload as separate pieces (sendmmsg
+ * iovecs, or a NIC gather list) and for host round trips, which then copy back 16 bytes per
+ * packet instead of the header span; in-place rewriting of 64-byte frames costs the path the
+ * partial 128-byte lines it dirties. */
+int upe_gpu_process_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                         uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n, void *stream);
+
+/* Apply one record to its frame (host; src/worker.c:174-176,197-200,213,227-230 as bytes). */
+void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec);
+
 /* Host round trip: process n packets that live in HOST memory, the way the path runs between
  * libpcap (reference src/rx_pcap.c:42-93 fills pktbufs in host memory) and AF_PACKET TX
  * (src/tx_afpacket.c:78-118 sends from host memory).  The batch is cut into chunks of `chunk`
@@ -248,6 +278,10 @@ int upe_gpu_host_free(void *ptr);
 int upe_gpu_process_batches(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
                             const uint64_t *d_desc, uint32_t *d_verdict, size_t n, size_t count,
                             void *stream);
+/* The same in emit mode (every batch writes its records to d_hdr). */
+int upe_gpu_process_batches_emit(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
+                                 const uint64_t *d_desc, uint32_t *d_verdict,
+                                 upe_hdr_rec_t *d_hdr, size_t n, size_t count, void *stream);
 
 /* upe_gpu_process() plus software RSS in the same pass (reference src/rx_pcap.c:67-77 parses
  * every packet a second time on the RX thread for this): d_flow_hash[i] (device, n uint32) =
@@ -363,5 +397,6 @@ UPE_STATIC_ASSERT(offsetof(upe_arp_entry_t, valid) == 24, "arp_entry_t.valid");
 UPE_STATIC_ASSERT(sizeof(upe_ndp_entry_t) == 40, "ndp_entry_t layout");
 UPE_STATIC_ASSERT(offsetof(upe_ndp_entry_t, valid) == 32, "ndp_entry_t.valid");
 UPE_STATIC_ASSERT(sizeof(upe_rule_stat_t) == 16, "rule_stat_t layout");
+UPE_STATIC_ASSERT(sizeof(upe_hdr_rec_t) == 16, "upe_hdr_rec_t layout");
 
 #endif /* UPE_GPU_H */

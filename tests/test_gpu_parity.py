@@ -21,20 +21,26 @@ from upe_amd.layout import COUNTERS_DTYPE, L1_DTYPE, V_CONSUMED, V_FWD
 pytestmark = pytest.mark.gpu
 
 
-def _run(worker_factory, wl, batches=1):
+def _run(worker_factory, wl, batches=1, emit=False):
+    """emit: the batch runs in emit mode and the frames come back with upe_hdr_apply applied."""
     w = worker_factory(wl.capacity)
     try:
         w.configure(wl)
         if batches == 1:
-            frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w)
+            frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w, emit=emit)
         else:
             frames = wl.frames.copy()
             verdict = np.zeros(wl.n, np.uint32)
             bounds = np.linspace(0, wl.n, batches + 1).astype(int)
             for s, e in zip(bounds[:-1], bounds[1:]):
                 b = gpu.DeviceBatch(w, frames, wl.desc[s:e])
-                b.run()
-                frames, verdict[s:e] = b.fetch()
+                if emit:
+                    b.run_emit()
+                    frames, verdict[s:e] = b.fetch()
+                    frames = gpu.hdr_apply(frames, wl.desc[s:e], b.fetch_hdr())
+                else:
+                    b.run()
+                    frames, verdict[s:e] = b.fetch()
                 b.free()
             counters, stats = w.get_stats()
             l1 = w.get_l1()
@@ -62,11 +68,47 @@ def _assert_same(got, ref, what="", batch_relative=False):
     assert l1.tobytes() == np.asarray(ref["l1"]).tobytes(), f"{what}: L1 state differs"
 
 
+@pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
                                   "config_d_small"])
-def test_golden_no_control(gpu_worker_factory, case):
+def test_golden_no_control(gpu_worker_factory, case, emit):
     wl, ref = golden_io.load(case)
-    _assert_same(_run(gpu_worker_factory, wl), ref, case)
+    _assert_same(_run(gpu_worker_factory, wl, emit=emit), ref, f"{case} emit={emit}")
+
+
+@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "config_d_small",
+                                  "edge_inconsistent"])
+def test_emit_records_exact(gpu_worker_factory, case):
+    """Emit mode: every record equals the one the reference's rewritten frame defines (zero for
+    packets not forwarded), and the frames stay as they were (ARP replies aside)."""
+    from test_emit_records import records_from_reference
+
+    wl, ref = golden_io.load(case)
+    if case.startswith("edge"):
+        r = oracle.run_restated(wl, apply_control=False)
+        ref = {"verdict": r.verdict, "frames": r.frames}
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        b = gpu.DeviceBatch(w, wl.frames, wl.desc)
+        b.run_emit()
+        frames, verdict = b.fetch()
+        rec = b.fetch_hdr()
+        b.free()
+    finally:
+        w.close()
+    assert np.array_equal(verdict, ref["verdict"])
+    want = records_from_reference(wl.frames, ref["frames"], wl.desc, ref["verdict"])
+    bad = np.nonzero((rec != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} records differ, first {bad[:8].tolist()}"
+    replied = (verdict & 0x40) != 0
+    from upe_amd.layout import desc_offsets
+
+    offs = desc_offsets(wl.desc)
+    keep = np.ones(len(frames), bool)
+    for o in offs[replied]:
+        keep[o:o + 48] = False
+    assert np.array_equal(frames[keep], wl.frames[keep]), "emit mode wrote into the frames"
 
 
 @pytest.mark.parametrize("case", ["edge_zero", "edge_consistent", "edge_inconsistent"])
@@ -87,23 +129,25 @@ def test_golden_edge_segmented(gpu_worker_factory, case):
     assert np.array_equal(ndp[keep], ref["ndp"][keep])
 
 
+@pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("case", ["edge_zero", "edge_consistent", "edge_inconsistent"])
-def test_edge_one_segment_vs_oracle(gpu_worker_factory, case):
+def test_edge_one_segment_vs_oracle(gpu_worker_factory, case, emit):
     """The same frames as ONE batch (control writes deferred): equals the oracle run with
     control replay off — exercises the L1 repair path with control packets in the batch."""
     wl, _ = golden_io.load(case)
     r = oracle.run_restated(wl, apply_control=False)
-    got = _run(gpu_worker_factory, wl)
+    got = _run(gpu_worker_factory, wl, emit=emit)
     _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                        "rule_stats": r.rule_stats, "l1": r.l1}, case)
 
 
+@pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("batches", [2, 7, 33])
-def test_multi_batch_l1_carry(gpu_worker_factory, batches):
+def test_multi_batch_l1_carry(gpu_worker_factory, batches, emit):
     """L1 caches, counters and rule_stats carry across batches exactly as across bursts."""
     wl, ref = golden_io.load("config_c_small")
-    _assert_same(_run(gpu_worker_factory, wl, batches=batches), ref, f"{batches} batches",
-                 batch_relative=True)
+    _assert_same(_run(gpu_worker_factory, wl, batches=batches, emit=emit), ref,
+                 f"{batches} batches", batch_relative=True)
 
 
 def _force_dst(wl, count, v4_ip=None, v6_ip=None):
@@ -121,7 +165,8 @@ def _force_dst(wl, count, v4_ip=None, v6_ip=None):
             fr[o + 38:o + 54] = v6_ip
 
 
-def test_random_l1_starts(gpu_worker_factory):
+@pytest.mark.parametrize("emit", [False, True])
+def test_random_l1_starts(gpu_worker_factory, emit):
     """Starting L1 entries that agree / disagree with the tables (or are absent from them), with
     the first packets of the batch sent to those destinations so the repair path runs."""
     rng = np.random.default_rng(11)
@@ -140,7 +185,7 @@ def test_random_l1_starts(gpu_worker_factory):
         wl.l1 = l1
         _force_dst(wl, 40 + 10 * trial, int(l1["last_arp_ip"][0]), l1["last_ndp_ip"][0])
         r = oracle.run_restated(wl)
-        got = _run(gpu_worker_factory, wl)
+        got = _run(gpu_worker_factory, wl, emit=emit)
         _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                            "rule_stats": r.rule_stats, "l1": r.l1}, f"trial {trial}")
         assert np.count_nonzero(r.verdict & 0x80) > 0
@@ -189,18 +234,21 @@ def _sha(*arrays):
     return h.hexdigest()
 
 
-@pytest.mark.parametrize("key,make", [
-    ("B_1M", lambda: synth.config_b()),
-    ("C_1M", lambda: synth.config_c()),
-    ("D_256k_64k_rules", lambda: synth.config_d(n=1 << 18)),
+@pytest.mark.parametrize("key,make,emit", [
+    ("B_1M", lambda: synth.config_b(), False),
+    ("B_1M", lambda: synth.config_b(), True),
+    ("C_1M", lambda: synth.config_c(), False),
+    ("C_1M", lambda: synth.config_c(), True),
+    ("D_256k_64k_rules", lambda: synth.config_d(n=1 << 18), False),
+    ("D_256k_64k_rules", lambda: synth.config_d(n=1 << 18), True),
 ])
-def test_full_size_digest(gpu_worker_factory, key, make):
+def test_full_size_digest(gpu_worker_factory, key, make, emit):
     """BASELINE.json full sizes against SHA-256 digests of the reference worker's outputs."""
     dg = golden_io.digests()[key]
     wl = make()
     assert _sha(wl.frames, wl.desc, wl.rules, wl.arp, wl.ndp) == dg["inputs"], \
         "synthetic generator drifted (inputs differ from the ones the digest was made from)"
-    frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl)
+    frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl, emit=emit)
     assert np.bincount(verdict & 0xF, minlength=7).tolist() == dg["codes"]
     assert [int(x) for x in counters[0].tolist()] == dg["counters"]
     assert _sha(verdict) == dg["verdict"]
@@ -232,8 +280,9 @@ def test_config_d_full_properties(gpu_worker_factory):
         assert np.array_equal(v & 0xFFFFFF0F, r.verdict & 0xFFFFFF0F)
 
 
+@pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("first_hit", [None, 0, 777, 150_001, 299_999])
-def test_lookback_far_first_hit(gpu_worker_factory, first_hit):
+def test_lookback_far_first_hit(gpu_worker_factory, first_hit, emit):
     """A starting ARP entry that disagrees with the table and a batch aimed at it: every packet
     before the first miss-then-hit packet (placed far into the batch, or absent) must take the
     entry's MAC — the decoupled look-back across ~1200 tiles."""
@@ -255,7 +304,7 @@ def test_lookback_far_first_hit(gpu_worker_factory, first_hit):
         wl.frames[offs[first_hit] + 22] = 64     # TTL alive
         wl.frames[offs[first_hit] + 36:offs[first_hit] + 38] = [0, 53]  # dport 53 -> FWD rule
     r = oracle.run_restated(wl)
-    got = _run(gpu_worker_factory, wl)
+    got = _run(gpu_worker_factory, wl, emit=emit)
     _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                        "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")
 

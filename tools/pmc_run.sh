@@ -1,11 +1,13 @@
 #!/bin/bash
 # PMC passes over a bench config (each counter group in its own rocprofv3 run, kernel trace only,
 # as the MI355X guide prescribes: FETCH_SIZE and WRITE_SIZE cannot share a pass).
-#   tools/pmc_run.sh [config] [groups...]   groups: fetch write sq sq2 clk ta tcp
+#   tools/pmc_run.sh [config] [mode] [groups...]   mode: emit | inplace
+#   groups: fetch write sq sq2 clk ta tcp
 set -e
 cfg=${1:-B}; shift || true
+mode=${1:-emit}; shift || true
 groups=${*:-fetch write sq clk}
-steps="--steps 20 --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg"
+steps="--steps 20 --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg --mode $mode --no-other-mode"
 for g in $groups; do
   case $g in
     fetch) ctr="FETCH_SIZE" ;;
@@ -18,5 +20,5 @@ for g in $groups; do
     tcp) ctr="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" ;;
     tcc) ctr="TCC_HIT_sum TCC_MISS_sum" ;;
   esac
-  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_$cfg/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_$g.log 2>&1 || echo "pass $g failed rc=$?"
+  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${cfg}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_${mode}_$g.log 2>&1 || echo "pass $g failed rc=$?"
 done

@@ -12,10 +12,13 @@ import sys
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "B"
 packets = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+mode = sys.argv[3] if len(sys.argv) > 3 else "emit"      # emit | inplace
+tag = "true>" if mode == "emit" else "false>"             # upe_classify<tss, emit>
 vals = {}
 for name in ("fetch", "write"):
-    f = glob.glob(f"gpurun_out/pmc_{cfg}/{name}/p_counter_collection.csv")[0]
-    rows = [r for r in csv.DictReader(open(f)) if "upe_classify" in r["Kernel_Name"]]
+    f = glob.glob(f"gpurun_out/pmc_{cfg}_{mode}/{name}/p_counter_collection.csv")[0]
+    rows = [r for r in csv.DictReader(open(f))
+            if "upe_classify" in r["Kernel_Name"] and tag in r["Kernel_Name"]]
     # only the full-batch launches (the bench's host leg launches smaller chunks)
     gmax = max(int(r["Grid_Size"]) for r in rows)
     acc = collections.defaultdict(float)
@@ -26,10 +29,11 @@ for name in ("fetch", "write"):
     vals[name] = v[len(v) // 2]           # median dispatch
 read_b = 2 * vals["fetch"] * 1024
 write_b = vals["write"] * 1024
-out = {"config": cfg, "packets": packets, "fetch_size_kb": vals["fetch"],
+out = {"config": cfg, "mode": mode, "packets": packets, "fetch_size_kb": vals["fetch"],
        "write_size_kb": vals["write"], "read_bytes": read_b, "write_bytes": write_b,
        "traffic_bytes_per_launch": read_b + write_b,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                  "bench.py (kernel trace only); read = 2 x FETCH_SIZE (gfx950), median dispatch"}
-json.dump(out, open(f"profiles/pmc_config{cfg}.json", "w"), indent=1)
+json.dump(out, open(f"profiles/pmc_config{cfg}{'_emit' if mode == 'emit' else ''}.json", "w"),
+          indent=1)
 print(json.dumps(out))

@@ -228,6 +228,7 @@ struct Args {
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
     uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
+    uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
 };
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
@@ -704,6 +705,7 @@ __device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len,
 // batch.  Every read is issued before any result is used, so the fold costs one memory round
 // trip (plus one per 1024 words of small-table rule_stats), not one per word.
 // ------------------------------------------------------------------------------------------
+template <bool kEmit>
 __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, bool look6) {
     __shared__ unsigned long long t_cnt[C_N];
     __shared__ uint32_t t_min[M_N], t_max[X_N];
@@ -821,7 +823,9 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
                     uint8_t* p = a.frames + (a.desc[i] >> 16);
                     const int fam = (p[12] == 0x86 && p[13] == 0xDD) ? 1 : 0;
                     if (!((fam_ok >> fam) & 1u) || i >= f[fam]) continue;
-                    uint32_t* w = reinterpret_cast<uint32_t*>(p);
+                    // emit mode: the packet's record holds the rewritten bytes 0..11
+                    uint32_t* w = kEmit ? reinterpret_cast<uint32_t*>(a.hdr + i)
+                                        : reinterpret_cast<uint32_t*>(p);
                     w[0] = lo[fam];
                     w[1] = hi[fam] | (a.port_mac_lo << 16);
                     w[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
@@ -873,7 +877,10 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
 // ------------------------------------------------------------------------------------------
 // classify: persistent workgroups over 256-packet tiles
 // ------------------------------------------------------------------------------------------
-template <bool kTssMode>
+// kEmit: the rewritten header bytes of forwarded packets go to a record per packet (a.hdr,
+// upe_hdr_rec_t, one coalesced 16-byte store per lane) and the frames are only read; otherwise
+// frames are rewritten in place (bytes 0..31 of each forwarded frame).
+template <bool kTssMode, bool kEmit>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6, cand bits
@@ -1106,7 +1113,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (hit) flags |= UPE_VF_NEIGH_HIT;
 
         // ---- write back ----
-        if (live && !(kAblate & 8)) {
+        if (kEmit && live && !(kAblate & 8)) {
+            // record: bytes 0..11 as forwarded (neighbour + port MAC on a hit, else unchanged),
+            // the new TTL / hop limit, the new IPv4 checksum, the family; zero unless forwarded
+            uint4 rec = make_uint4(0, 0, 0, 0);
+            if (code == UPE_V_FWD) {
+                rec.x = hit ? mlo : w[0];
+                rec.y = hit ? (mhi | (a.port_mac_lo << 16)) : w[1];
+                rec.z = hit ? ((a.port_mac_lo >> 16) | (a.port_mac_hi << 16)) : w[2];
+                rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
+                             : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
+            }
+            a.hdr[i] = rec;
+        } else if (live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
                 store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
@@ -1284,7 +1303,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // the other waves wait here, so the last workgroup folds the batch with all its threads
     __syncthreads();
     if (!s_last) return;
-    batch_tail(a, tid, look4, look6);
+    batch_tail<kEmit>(a, tid, look4, look6);
     STAMP(8);
 }
 
@@ -2195,17 +2214,18 @@ int upe_gpu_get_l1(upe_gpu_ctx_t* c, upe_l1_state_t* l1) {
     return 0;
 }
 
-int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
-                    uint32_t* d_verdict, size_t n, void* stream) {
-    return upe_gpu_process_rss(c, d_frames, d_desc, d_verdict, nullptr, n, stream);
-}
+}  // extern "C"
 
-int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
-                        uint32_t* d_verdict, uint32_t* d_flow_hash, size_t n, void* stream) {
+namespace {
+// One batch: the classify launch (in place, or emit mode when d_hdr is given), plus the
+// rule_stats group-by for tables over kLdsStatsMax rules.
+int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
+                 uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
     if (((uintptr_t)d_frames & 15u) != 0) return fail("frames buffer must be 16-byte aligned");
+    if (((uintptr_t)d_hdr & 15u) != 0) return fail("header records must be 16-byte aligned");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
@@ -2261,6 +2281,8 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
     a.stats = c->stats;
     a.stats_idx = c->stats_idx;
     a.flow_hash = d_flow_hash;
+    a.hdr = reinterpret_cast<uint4*>(d_hdr);
+    const bool emit = d_hdr != nullptr && n > 0;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     a.lens16 = nullptr;
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
@@ -2285,17 +2307,21 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
         c->resident_tss = c->tss;
         int per_cu = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, c->tss ? upe_classify<true> : upe_classify<false>, kBlock, lds));
+            &per_cu, c->tss ? upe_classify<true, false> : upe_classify<false, false>, kBlock, lds));
         if (per_cu < 1) per_cu = 1;
         if (c->blocks_per_cu_override > 0) per_cu = c->blocks_per_cu_override;
         c->resident = (uint32_t)per_cu * (uint32_t)c->cus;
         c->resident_lds = lds;
     }
     const uint32_t grid = ntiles == 0 ? 1u : ntiles < c->resident ? ntiles : c->resident;
-    if (c->tss)
-        hipLaunchKernelGGL(upe_classify<true>, dim3(grid), dim3(kBlock), lds, s, a);
+    if (c->tss && emit)
+        hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a);
+    else if (c->tss)
+        hipLaunchKernelGGL((upe_classify<true, false>), dim3(grid), dim3(kBlock), lds, s, a);
+    else if (emit)
+        hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a);
     else
-        hipLaunchKernelGGL(upe_classify<false>, dim3(grid), dim3(kBlock), lds, s, a);
+        hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
     HIP_TRY(hipGetLastError());
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
@@ -2327,6 +2353,25 @@ int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_d
     }
     c->have_batch = true;
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int upe_gpu_process(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                    uint32_t* d_verdict, size_t n, void* stream) {
+    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, nullptr, n, stream);
+}
+
+int upe_gpu_process_rss(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                        uint32_t* d_verdict, uint32_t* d_flow_hash, size_t n, void* stream) {
+    return process_impl(c, d_frames, d_desc, d_verdict, d_flow_hash, nullptr, n, stream);
+}
+
+int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                         uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
+    if (n && !d_hdr) return fail("null header records");
+    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
 }
 
 int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
@@ -2439,6 +2484,17 @@ int upe_gpu_process_batches(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list, con
     if (count && !d_frames_list) return fail("null frames list");
     for (size_t k = 0; k < count; ++k)
         if (upe_gpu_process(c, d_frames_list[k], d_desc, d_verdict, n, stream) != 0) return -1;
+    return 0;
+}
+
+int upe_gpu_process_batches_emit(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list,
+                                 const uint64_t* d_desc, uint32_t* d_verdict, upe_hdr_rec_t* d_hdr,
+                                 size_t n, size_t count, void* stream) {
+    if (!c) return fail("null context");
+    if (count && !d_frames_list) return fail("null frames list");
+    for (size_t k = 0; k < count; ++k)
+        if (upe_gpu_process_emit(c, d_frames_list[k], d_desc, d_verdict, d_hdr, n, stream) != 0)
+            return -1;
     return 0;
 }
 

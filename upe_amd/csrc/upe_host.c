@@ -13,6 +13,8 @@
  *   upe_pcap_read       the capture side of reference src/rx_pcap.c:42-93 / 95-167 for a pcap
  *                       file: every record in file order, caplen > PKTBUF_DATA_SIZE (2048)
  *                       dropped (src/rx_pcap.c:53-57), the rest packed at 16-byte aligned offsets.
+ *   upe_hdr_apply       an emit-mode record (upe_hdr_rec_t) applied to its frame: the rewrite of
+ *                       src/worker.c:162-244 as bytes.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -313,4 +315,21 @@ int upe_pcap_read(const char *path, uint8_t *frames, size_t frames_cap, uint64_t
     info->frames_bytes = cursor + UPE_FRAME_TAIL;
     if (rc == 0 && fill) memset(frames + cursor, 0, UPE_FRAME_TAIL);
     return rc;
+}
+
+/* ---- emit-mode records ------------------------------------------------------------------- */
+
+/* The bytes process_packet leaves in a forwarded frame (reference src/worker.c:174-176 TTL and
+ * checksum, :197-200 / :227-230 MACs, :213 hop limit), from a upe_hdr_rec_t. */
+void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec) {
+    const uint8_t fam = rec->b[15];
+    if (fam != 4 && fam != 6) return;
+    memcpy(frame, rec->b, 12);
+    if (fam == 4) {
+        frame[22] = rec->b[12];
+        frame[24] = rec->b[13];
+        frame[25] = rec->b[14];
+    } else {
+        frame[21] = rec->b[12];
+    }
 }

@@ -61,6 +61,9 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_rss": (I, [P, P, P, P, P, SZ, P]),
         "upe_gpu_compact": (I, [P, P, SZ, ctypes.c_uint32, P, P, P]),
         "upe_gpu_process_segmented": (I, [P, P, P, P, SZ, P, SZ, P, SZ, ctypes.c_int64, P, P]),
+        "upe_gpu_process_emit": (I, [P, P, P, P, P, SZ, P]),
+        "upe_gpu_process_batches_emit": (I, [P, P, P, P, P, SZ, SZ, P]),
+        "upe_hdr_apply": (None, [P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
     }
@@ -87,7 +90,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_g
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
-            "upe_gpu_process_segmented",
+            "upe_gpu_process_segmented", "upe_gpu_process_emit", "upe_gpu_process_batches_emit",
+            "upe_hdr_apply",
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free")
@@ -189,6 +193,20 @@ class GpuWorker:
         _check(LIB.upe_gpu_process(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
                                    _dev_ptr(verdict), n, stream or None),
                "upe_gpu_process")
+
+    def process_emit(self, frames, desc, verdict, hdr, n: int, stream=None) -> None:
+        """Emit mode: rewritten header bytes into `hdr` (n 16-byte records), frames read only."""
+        _check(LIB.upe_gpu_process_emit(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
+                                        _dev_ptr(verdict), _dev_ptr(hdr), n, stream or None),
+               "upe_gpu_process_emit")
+
+    def process_batches_emit(self, frames_ptrs, desc, verdict, hdr, n: int, stream=None) -> None:
+        """process_batches in emit mode (every batch writes its records to `hdr`)."""
+        arr = (ctypes.c_void_p * len(frames_ptrs))(*[int(x) for x in frames_ptrs])
+        _check(LIB.upe_gpu_process_batches_emit(self._ctx, arr, _dev_ptr(desc), _dev_ptr(verdict),
+                                                _dev_ptr(hdr), n, len(frames_ptrs),
+                                                stream or None),
+               "upe_gpu_process_batches_emit")
 
     def process_batches(self, frames_ptrs, desc, verdict, n: int, stream=None) -> None:
         """Queue len(frames_ptrs) batches (device pointers) back to back from native code."""
@@ -351,8 +369,16 @@ class DeviceBatch:
             worker.h2d(self.desc, np.ascontiguousarray(desc))
         worker.sync()
 
+        self.hdr = 0
+
     def run(self, stream=None) -> None:
         self.worker.process(self.frames, self.desc, self.verdict, self.n, stream)
+
+    def run_emit(self, stream=None) -> None:
+        """Emit mode: records into a device array owned by this batch."""
+        if not self.hdr:
+            self.hdr = self.worker.malloc(max(16 * self.n, 16))
+        self.worker.process_emit(self.frames, self.desc, self.verdict, self.hdr, self.n, stream)
 
     def fetch(self):
         """(frames, verdict) back to the host (synchronises)."""
@@ -365,23 +391,52 @@ class DeviceBatch:
         self.worker.sync()
         return frames, verdict
 
+    def fetch_hdr(self) -> np.ndarray:
+        """The emit-mode records, (n, 16) uint8 (synchronises)."""
+        self.worker.sync()
+        rec = np.empty((self.n, 16), np.uint8)
+        if self.n:
+            self.worker.d2h(rec, self.hdr)
+        self.worker.sync()
+        return rec
+
     def free(self) -> None:
-        for p in (self.frames, self.desc, self.verdict):
-            self.worker.free(p)
-        self.frames = self.desc = self.verdict = 0
+        for p in (self.frames, self.desc, self.verdict, self.hdr):
+            if p:
+                self.worker.free(p)
+        self.frames = self.desc = self.verdict = self.hdr = 0
 
 
-def run_workload(wl, device: int = 0, worker: GpuWorker | None = None):
+def hdr_apply(frames: np.ndarray, desc: np.ndarray, rec: np.ndarray) -> np.ndarray:
+    """upe_hdr_apply over a batch (through the C helper), returns the rewritten frames."""
+    from .layout import desc_offsets
+
+    out = np.ascontiguousarray(frames).copy()
+    rec = np.ascontiguousarray(rec, np.uint8).reshape(-1, 16)
+    base = out.ctypes.data
+    offs = desc_offsets(desc)
+    for i in np.nonzero(rec[:, 15] != 0)[0]:
+        LIB.upe_hdr_apply(ctypes.c_void_p(base + int(offs[i])), _np_ptr(rec[i]))
+    return out
+
+
+def run_workload(wl, device: int = 0, worker: GpuWorker | None = None, emit: bool = False):
     """Process a synth.Workload once on the GPU; returns (frames, verdict, counters,
-    rule_stats, l1) like oracle.Result."""
+    rule_stats, l1) like oracle.Result.  emit: run in emit mode and return the frames with the
+    records applied by upe_hdr_apply."""
     own = worker is None
     w = worker or GpuWorker(device, wl.capacity)
     try:
         if own:
             w.configure(wl)
         b = DeviceBatch(w, wl.frames, wl.desc)
-        b.run()
-        frames, verdict = b.fetch()
+        if emit:
+            b.run_emit()
+            frames, verdict = b.fetch()
+            frames = hdr_apply(frames, wl.desc, b.fetch_hdr())
+        else:
+            b.run()
+            frames, verdict = b.fetch()
         b.free()
         counters, stats = w.get_stats()
         l1 = w.get_l1()
