@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -145,6 +146,82 @@ __global__ void __launch_bounds__(256) coalesced(const uint4* frames, const uint
     verdict[i] = h;
 }
 
+
+// ---- compute + record store variants: every packet also costs ~kWork VALU ops (4 chains) and
+// stores a 16-byte record plus its verdict, as the classify kernel does in emit mode ----------
+constexpr int kWork = 48;
+__device__ __forceinline__ uint4 crunch(const uint4 (&v)[4], uint32_t i) {
+    uint32_t a = v[0].x ^ i, b = v[1].y, c = v[2].z, d = v[3].w;
+#pragma unroll
+    for (int k = 0; k < kWork; ++k) {
+        a = a * 0x9E3779B1u + v[k & 3].x;
+        b = (b ^ (b >> 7)) + v[(k + 1) & 3].y;
+        c = c * 0x85EBCA77u + v[(k + 2) & 3].z;
+        d = (d << 3) ^ v[(k + 3) & 3].w;
+    }
+    return make_uint4(a, b, c, d);
+}
+
+template <bool kFlat>
+__global__ void __launch_bounds__(256) work_plain(const uint8_t* frames, const uint64_t* desc,
+                                                  uint32_t* verdict, uint4* rec, uint32_t n) {
+    const uint32_t nt = (n + 255) / 256;
+    for (uint32_t t = blockIdx.x; t < nt; t += kFlat ? nt : gridDim.x) {
+        const uint32_t i = t * 256 + threadIdx.x;
+        if (i >= n) break;
+        const uint64_t d = desc[i];
+        const uint4* q = reinterpret_cast<const uint4*>(frames + ((d >> 20) << 4));
+        uint4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = q[c];
+        const uint4 r = crunch(v, i);
+        rec[i] = r;
+        verdict[i] = r.x ^ r.w;
+    }
+}
+
+// one-deep software pipeline, branch-free loads (dead lanes load the buffer's first bytes), two
+// register sets used in turn (a copy between them would wait for the loads)
+__global__ void __launch_bounds__(256) work_pipe(const uint8_t* frames, const uint64_t* desc,
+                                                 uint32_t* verdict, uint4* rec, uint32_t n) {
+    const uint32_t nt = (n + 255) / 256;
+    const uint32_t G = gridDim.x;
+    uint32_t t = blockIdx.x;
+    if (t >= nt) return;
+    auto idx = [&](uint32_t tt) {
+        const uint32_t i = tt * 256 + threadIdx.x;
+        return tt < nt && i < n ? i : 0u;
+    };
+    auto load = [&](uint64_t d, uint4 (&w)[4]) {
+        const uint4* q = reinterpret_cast<const uint4*>(frames + ((d >> 20) << 4));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[c] = q[c];
+    };
+    auto work = [&](uint32_t tt, const uint4 (&w)[4]) {
+        const uint32_t i = tt * 256 + threadIdx.x;
+        const uint4 r = crunch(w, i);
+        if (i < n) {
+            rec[i] = r;
+            verdict[i] = r.x ^ r.w;
+        }
+    };
+    uint4 A[4], B[4];
+    uint64_t dB = desc[idx(t + G)];
+    load(desc[idx(t)], A);
+    for (;;) {
+        const uint64_t dA = desc[idx(t + 2 * G)];
+        load(dB, B);
+        work(t, A);
+        t += G;
+        if (t >= nt) break;
+        dB = desc[idx(t + 2 * G)];
+        load(dA, A);
+        work(t, B);
+        t += G;
+        if (t >= nt) break;
+    }
+}
+
 struct Case {
     const char* name;
     void (*launch)(uint8_t*, const uint64_t*, uint32_t*, uint32_t, int, hipStream_t);
@@ -162,6 +239,16 @@ template <int S>
 void L_persist_pf(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int g, hipStream_t s) {
     hipLaunchKernelGGL(persist_pf<S>, dim3(g), dim3(256), 0, s, f, d, v, n);
 }
+uint4* g_rec_host;
+void L_work_flat(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int, hipStream_t s) {
+    hipLaunchKernelGGL(work_plain<true>, dim3((n + 255) / 256), dim3(256), 0, s, f, d, v, g_rec_host, n);
+}
+void L_work_persist(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int g, hipStream_t s) {
+    hipLaunchKernelGGL(work_plain<false>, dim3(g), dim3(256), 0, s, f, d, v, g_rec_host, n);
+}
+void L_work_pipe(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int g, hipStream_t s) {
+    hipLaunchKernelGGL(work_pipe, dim3(g), dim3(256), 0, s, f, d, v, g_rec_host, n);
+}
 void L_coal(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int, hipStream_t s) {
     hipLaunchKernelGGL(coalesced, dim3((n + 255) / 256), dim3(256), 0, s, (const uint4*)f,
                        (const uint4*)d, v, n);
@@ -170,6 +257,7 @@ void L_coal(uint8_t* f, const uint64_t* d, uint32_t* v, uint32_t n, int, hipStre
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
     const int reps = argc > 2 ? atoi(argv[2]) : 100;
+    const char* only = argc > 3 ? argv[3] : nullptr;   // substring filter of case names
     const size_t fb = (size_t)n * 64 + 256;
     int copies = (int)((12ull << 30) / fb);
     if (copies > 220) copies = 220;
@@ -184,6 +272,7 @@ int main(int argc, char** argv) {
     uint4* outp;
     CK(hipMalloc(&outp, (size_t)n * 32));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_out), &outp, sizeof outp));
+    g_rec_host = outp;
     std::vector<uint64_t> hd(n);
     for (uint32_t i = 0; i < n; ++i) hd[i] = ((uint64_t)i * 64) << 16 | 64;
     CK(hipMemcpy(desc, hd.data(), (size_t)n * 8, hipMemcpyHostToDevice));
@@ -193,6 +282,10 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const Case cases[] = {
+        {"flat_out16_all", L_flat<8>},
+        {"work_flat", L_work_flat},
+        {"pwork_plain", L_work_persist},
+        {"pwork_pipe", L_work_pipe},
         {"coalesced_read", L_coal},
         {"flat_read", L_flat<0>},
         {"flat_st32_half", L_flat<1>},
@@ -209,11 +302,12 @@ int main(int argc, char** argv) {
         {"persist_pf_st32_half", L_persist_pf<1>},
         {"persist_pf_st64_half", L_persist_pf<2>},
     };
-    const int grids[] = {1024, 2048};
+    const int grids[] = {1024, 1280};
     printf("n=%u copies=%d reps=%d (us per launch; GB/s of desc+frames+verdict)\n", n, copies,
            reps);
     for (const Case& c : cases) {
         const bool per = c.name[0] == 'p';
+        if (only && !strstr(c.name, only)) continue;
         for (int gi = 0; gi < (per ? 2 : 1); ++gi) {
             const int g = grids[gi];
             for (int k = 0; k < 5; ++k) c.launch(pool + (size_t)(k % copies) * fb, desc, verdict, n, g, s);

@@ -11,20 +11,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from upe_amd import gpu, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+emit = (sys.argv[2] if len(sys.argv) > 2 else "emit") == "emit"
 wl = synth.config_b(n=n)
 w = gpu.GpuWorker(0, wl.capacity)
 w.configure(wl)
 dev = torch.device("cuda", 0)
-frames = [torch.from_numpy(wl.frames).to(dev) for _ in range(4)]
+frames = [torch.from_numpy(wl.frames).to(dev) for _ in range(6)]
 desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
 verdict = torch.empty(n, dtype=torch.int32, device=dev)
+hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 lib = gpu.LIB
 lib.upe_gpu_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 names = ["entry", "init", "win", "scan", "loop", "flush", "wait", "ticket", "tail", "reduced", "barrier"]
-for rep in range(4):
+for rep in range(6):
     buf = np.zeros(8192 * 16, np.uint64)
     lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), 0)  # no-op read
-    w.process(frames[rep], desc, verdict, n)
+    if emit:
+        w.process_emit(frames[rep], desc, verdict, hdr, n)
+    else:
+        w.process(frames[rep], desc, verdict, n)
     w.sync()
     lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes)
     ntiles = (n + 255) // 256

@@ -92,7 +92,8 @@ constexpr int kShards = 8;             // arrival-ticket shards
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
-// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify
+// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 128 no arrival
+// ticket and no last-workgroup repair, 256 no fold of the previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
 // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt not waited (gfx9 encoding)
 constexpr int kWaitVm0 = 0x0F70;
@@ -116,9 +117,8 @@ struct __attribute__((aligned(16))) RuleV6 {
     uint32_t s[3], sm[3], d[3], dm[3], pad[4];
 };
 
-// L1 state in word form (device resident between batches) + whether each entry agrees with the
-// current neighbour snapshot (maintained by every batch's last workgroup and by upe_refresh
-// after every table / L1 upload).
+// L1 state in word form + whether each entry agrees with the current neighbour snapshot.
+// DevState keeps two, by batch parity (see "Sequential state between batches").
 struct DevL1 {
     uint32_t arp_ip, arp_mac_lo, arp_mac_hi;
     uint32_t ndp_ip[4];
@@ -127,21 +127,31 @@ struct DevL1 {
     uint32_t pad[5];
 };
 
-// Per-batch accumulators.  Every workgroup adds its totals with device atomics into replica
-// (workgroup % kReps); the batch's last workgroup reads them back with atomic exchanges, which
-// also re-arm them for the next batch.
-enum { C_PARSED, C_MATCHED, C_FWD, C_DROPPED, C_CONSUMED, C_ARP_LEARN, C_ARP_REPLY, C_CTRL,
-       C_CAND, C_N };   // C_CAND: workgroups holding packets a disagreeing start entry may answer
-enum { M_F4, M_F6, M_CTRL, M_N };  // minima: first miss-then-hit per family, first control packet
-enum { X_M4, X_M6, X_N };          // maxima: last table hit per family (index + 1, 0 = none)
-constexpr int kAccFields = C_N + M_N + X_N;
-struct BatchAcc {
-    uint32_t cnt[kReps][C_N];
-    uint32_t mins[kReps][M_N];
-    uint32_t maxs[kReps][X_N];
+// ---- Sequential state between batches ------------------------------------------------------
+// Nothing is folded at the end of a launch (no last-workgroup fold, no grid-wide wait): every
+// workgroup adds what it saw into replicated accumulators (replica = workgroup % kReps) and the
+// NEXT launch, in its first instructions, folds the previous batch's L1 outcome into the state
+// it starts from.  Batch k (the context's k-th launch) uses
+//   l1[k % 2]       the L1 state after batch k - 2 (read)
+//   acc[(k - 1) % 3] batch k - 1's minima / maxima and pay[(k - 1) % 2] its last-hit payloads
+//                    (read: every workgroup folds them into its own starting L1 entry)
+//   l1[(k + 1) % 2] the state after batch k - 1 (written by workgroup 0, for batch k + 1)
+//   acc[k % 3]      this batch's accumulators, pay[k % 2] its payloads (written)
+//   acc[(k + 1) % 3] re-armed by workgroup 0 for batch k + 1
+// Host calls that read or replace the L1 state first fold the pending batch the same way
+// (upe_l1_sync).  Counters go straight into replicated cumulative totals, rule_stats into
+// replicated per-sorted-index totals; the host sums replicas when it reads them.
+enum { C_PARSED, C_MATCHED, C_FWD, C_DROPPED, C_CONSUMED, C_ARP_LEARN, C_ARP_REPLY, C_CTRL, C_N };
+struct __attribute__((aligned(128))) BatchAcc {
+    uint32_t cnt[kReps][C_N];   // this batch's counters
+    uint4 l1r[kReps];           // x, y: first miss-then-hit index v4 / v6 (min, kNone = none);
+                                // z, w: last table hit v4 / v6 (max of index + 1, 0 = none)
+    uint32_t ctrl[kReps];       // first control packet (min)
+    uint32_t grid;              // the batch's grid (which workgroup holds a payload)
+    uint32_t pad[31];
 };
-// Payload of a workgroup's last table hit per family; the last workgroup reads the one the batch
-// maximum points at.  Written with agent-scope (sc1) stores before the arrival ticket.
+// Payload of a workgroup's last table hit per family; the next batch reads the one the batch
+// maximum points at.
 struct __attribute__((aligned(64))) TilePay {
     uint32_t m4_dst, m4_mac_lo, m4_mac_hi;
     uint32_t m6_dst[4], m6_mac_lo, m6_mac_hi;
@@ -155,21 +165,15 @@ struct Tickets {
     uint32_t top[32];
 };
 
-// Accumulated worker state.
-struct DevTotals {
-    unsigned long long cnt[8];     // upe_counters_t order
-    unsigned long long n_ctrl, first_ctrl;
-    unsigned long long batch[8];
-};
-
 // Everything a batch reads or writes besides the packets and the tables, in one device
-// allocation reached through one kernel argument (keeps the kernel's scalar registers free).
+// allocation.
 struct DevState {
-    DevL1 l1;
-    DevTotals totals;
-    BatchAcc acc;
+    DevL1 l1[2];
+    BatchAcc acc[3];
     Tickets tickets;
+    unsigned long long totals[kReps][8];                    // cumulative, upe_counters_t order
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
+    uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
     uint32_t* cand_tile;             // [ntiles], zero between batches
     unsigned long long* stats;       // [cap][2] worker rule_stats (mid-size and large tables)
@@ -229,6 +233,14 @@ struct Args {
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
     uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
+    // this batch's slots of the between-batch state (DevState comment)
+    const DevL1* l1_in;
+    DevL1* l1_out;
+    BatchAcc* acc_cur;
+    const BatchAcc* acc_prev;
+    BatchAcc* acc_next;
+    const TilePay* pay_prev;
+    uint32_t* census;                // non-null: a residency census launch (census_probe) only
 };
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
@@ -403,6 +415,50 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 template <typename V, typename T>
 __device__ __forceinline__ const __attribute__((address_space(4))) V* as_const(const T* p) {
     return (const __attribute__((address_space(4))) V*)p;
+}
+
+// The L1 state after a batch (src/worker.c:186-195, 218-225): the state
+// before it, unless some forwarded packet missed the starting entry and hit the table — then
+// the batch's last table hit, whose MAC is the table's (so the entry agrees with the table).
+// in: DevL1 words before the batch; f4 / f6: first miss-then-hit (kNone = none); m4 / m6: last
+// table hit + 1 (0 = none); grid / pay: the batch's grid and per-workgroup last-hit payloads.
+// All arguments wave-uniform.  L: DevL1 words 0..10 after the batch.
+__device__ __forceinline__ void fold_l1(const u32x16& in, uint32_t f4, uint32_t f6, uint32_t m4,
+                                        uint32_t m6, uint32_t grid, const TilePay* pay,
+                                        uint32_t (&L)[11]) {
+#pragma unroll
+    for (int j = 0; j < 11; ++j) L[j] = in[j];
+    if (f4 != kNone && m4 != 0) {
+        const u32x16 P = *as_const<u32x16>(pay + ((m4 - 1) / kTile) % grid);
+        L[0] = P[0]; L[1] = P[1]; L[2] = P[2];
+        L[9] = 1;
+    }
+    if (f6 != kNone && m6 != 0) {
+        const u32x16 P = *as_const<u32x16>(pay + ((m6 - 1) / kTile) % grid);
+        L[3] = P[3]; L[4] = P[4]; L[5] = P[5]; L[6] = P[6]; L[7] = P[7]; L[8] = P[8];
+        L[10] = 1;
+    }
+}
+
+// Fold a finished batch into the state the next one starts from, on the host's request (before
+// the L1 state is read or replaced, or a neighbour table changes): l1 = fold(l1, acc, pay), and
+// acc's L1 fields back to "nothing happened", so the next launch's own fold is the identity.
+__global__ void upe_l1_sync(DevL1* l1, BatchAcc* acc, const TilePay* pay) {
+    const int lane = threadIdx.x;
+    uint4 pr = make_uint4(kNone, kNone, 0u, 0u);
+    if (lane < kReps) pr = acc->l1r[lane];
+    const uint32_t f4 = wave_reduce<1>(pr.x), f6 = wave_reduce<1>(pr.y);
+    const uint32_t m4 = wave_reduce<2>(pr.z), m6 = wave_reduce<2>(pr.w);
+    const u32x16 in = *as_const<u32x16>(l1);
+    uint32_t L[11];
+    fold_l1(in, f4, f6, m4, m6, acc->grid ? acc->grid : 1u, pay, L);
+    __syncthreads();
+    if (lane < kReps) acc->l1r[lane] = make_uint4(kNone, kNone, 0u, 0u);
+    if (lane == 0) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(l1);
+#pragma unroll
+        for (int j = 0; j < 11; ++j) w[j] = L[j];
+    }
 }
 
 // First-match scan (reference src/rule_table.c:163-176 over match_rule :76-91).  Every lane of
@@ -699,106 +755,32 @@ __device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len,
 }
 
 // ------------------------------------------------------------------------------------------
-// The batch's last workgroup (all its threads, every other workgroup has arrived): fold the
-// accumulators into the worker totals, update the L1 state, give the starting L1 entry's answer
-// to the packets it answered in the reference, and re-arm accumulators and tickets for the next
-// batch.  Every read is issued before any result is used, so the fold costs one memory round
-// trip (plus one per 1024 words of small-table rule_stats), not one per word.
+// The batch's last workgroup, when a starting L1 entry disagreed with the table (every other
+// workgroup has arrived): packets whose destination is that entry, before the batch's first
+// miss-then-hit packet of their family, took the entry's MAC in the reference
+// (src/worker.c:186-188, 218-220); their workgroups flagged the tiles and released their
+// stores.  anycand: some workgroup flagged a tile.  L1: the starting state (DevL1 words).
+// Re-arms the tickets.
 // ------------------------------------------------------------------------------------------
 template <bool kEmit>
-__device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, bool look6) {
-    __shared__ unsigned long long t_cnt[C_N];
-    __shared__ uint32_t t_min[M_N], t_max[X_N];
-    __shared__ unsigned long long t_st[2 * kSmallRules];
-    __shared__ uint32_t t_pay[kPayWords];
+__device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, bool look6,
+                                           bool anycand, const uint32_t (&L1)[11]) {
     DevState* S = a.st;
     const int lane = tid & 63;
-    const bool small = a.nrules_pad <= (uint32_t)kSmallRules;
-    const uint32_t E = 2 * a.nrules_pad;
-    if (tid < C_N) t_cnt[tid] = 0;
-    if (tid < M_N) t_min[tid] = kNone;
-    if (tid < X_N) t_max[tid] = 0;
-    for (uint32_t e = tid; e < 2 * kSmallRules; e += kBlock) t_st[e] = 0;
-    __syncthreads();
-
-    // accumulators: read and re-arm in one atomic exchange per word (reads the value every
-    // workgroup's atomics left, whichever XCD they ran on)
-    uint32_t* accw = reinterpret_cast<uint32_t*>(&S->acc);
-    constexpr uint32_t kCntW = kReps * C_N, kMinW = kReps * M_N, kAccW = kReps * kAccFields;
-    constexpr int kAccPer = (int)((kAccW + kBlock - 1) / kBlock);
-    uint32_t av[kAccPer];
-#pragma unroll
-    for (int j = 0; j < kAccPer; ++j) {
-        const uint32_t k = (uint32_t)tid + (uint32_t)j * kBlock;
-        const bool is_min = k >= kCntW && k < kCntW + kMinW;
-        av[j] = k < kAccW ? __hip_atomic_exchange(&accw[k], is_min ? kNone : 0u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                          : 0u;
-    }
-    // The workgroup that took the batch's last tile most likely holds the batch's last table
-    // hits: read its payload now, speculatively (used only if it is the right one).
-    const uint32_t spec = (a.ntiles - 1) % gridDim.x;
-    uint32_t pv = 0;
-    if (tid < kPayWords)
-        pv = __hip_atomic_load(reinterpret_cast<const uint32_t*>(&a.pay[spec]) + tid,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // small-table rule_stats replicas, kStPer words per thread per round
-    constexpr int kStPer = 4;
-    const uint32_t EW = small ? E * kReps : 0u;
-    for (uint32_t base = 0; base < EW; base += kStPer * kBlock) {
-        unsigned long long sv[kStPer];
-#pragma unroll
-        for (int j = 0; j < kStPer; ++j) {
-            const uint32_t k = base + (uint32_t)tid + (uint32_t)j * kBlock;
-            sv[j] = k < EW ? __hip_atomic_exchange(&S->acc_stats[k / E][k % E], 0ull,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < kStPer; ++j) {
-            const uint32_t k = base + (uint32_t)tid + (uint32_t)j * kBlock;
-            if (sv[j]) atomicAdd(&t_st[k % E], sv[j]);
-        }
-    }
-    if (tid < kPayWords) t_pay[tid] = pv;
-#pragma unroll
-    for (int j = 0; j < kAccPer; ++j) {
-        const uint32_t k = (uint32_t)tid + (uint32_t)j * kBlock;
-        const uint32_t v = av[j];
-        if (k >= kAccW) continue;
-        if (k < kCntW) {
-            if (v) atomicAdd(&t_cnt[k % C_N], (unsigned long long)v);
-        } else if (k < kCntW + kMinW) {
-            if (v != kNone) atomicMin(&t_min[(k - kCntW) % M_N], v);
-        } else {
-            if (v) atomicMax(&t_max[(k - kCntW - kMinW) % X_N], v);
-        }
-    }
-    __syncthreads();
-
-    // worker totals and this batch's summary
-    if (small && (uint32_t)tid < E && t_st[tid]) atomicAdd(&a.stats_idx[tid], t_st[tid]);
-    DevTotals* T = &S->totals;
-    if (tid < 8) {
-        // upe_counters_t order: pkts_in, then C_PARSED .. C_ARP_REPLY
-        const unsigned long long b = tid == 0 ? (unsigned long long)a.n : t_cnt[tid - 1];
-        if (b) atomicAdd(&T->cnt[tid], b);
-        T->batch[tid] = b;
-    }
-    if (tid == 8) T->n_ctrl = t_cnt[C_CTRL];
-    if (tid == 9)
-        T->first_ctrl = t_min[M_CTRL] == kNone ? ~0ull : (unsigned long long)t_min[M_CTRL];
-    if (tid >= 64) return;   // wave 0 does the rest
-
-    // Packets whose destination is the starting entry, before the first miss-then-hit packet of
-    // their family, took the entry's MAC (found) in the reference: src/worker.c:186-188, 218-220.
-    // Only flagged tiles are visited (their workgroups released their stores).
-    DevL1* L = &S->l1;
-    if ((look4 || look6) && t_cnt[C_CAND] != 0) {
+    if (tid >= 64) return;   // wave 0 does it
+    if (anycand) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const uint32_t f[2] = {t_min[M_F4], t_min[M_F6]};
-        const uint32_t lo[2] = {L->arp_mac_lo, L->ndp_mac_lo};
-        const uint32_t hi[2] = {L->arp_mac_hi, L->ndp_mac_hi};
+        // the batch's first miss-then-hit per family (every workgroup's atomics were performed
+        // before its ticket)
+        uint32_t x = kNone, y = kNone;
+        if (lane < kReps) {
+            const uint32_t* r = reinterpret_cast<const uint32_t*>(&a.acc_cur->l1r[lane]);
+            x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            y = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t f[2] = {wave_reduce<1>(x), wave_reduce<1>(y)};
+        const uint32_t lo[2] = {L1[1], L1[7]};
+        const uint32_t hi[2] = {L1[2], L1[8]};
         // nothing at or after the later of the two first-hit indexes needs the start entry
         const uint32_t fmax = max(look4 ? f[0] : 0u, look6 ? f[1] : 0u);
         const uint32_t tend = fmax == kNone ? a.ntiles : min(a.ntiles, fmax / kTile + 1);
@@ -837,41 +819,34 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
         for (uint32_t t = tend + (uint32_t)lane; t < a.ntiles; t += 64)
             __hip_atomic_store(&a.cand_tile[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-
-    // New L1 state: the last table hit, if some packet missed the starting entry and hit the
-    // table (from then on the cache only ever holds table answers, so it agrees with the
-    // table); otherwise unchanged.
-    if (lane == 0 && t_min[M_F4] != kNone && t_max[X_M4] != 0) {
-        const uint32_t wg = ((t_max[X_M4] - 1) / kTile) % gridDim.x;
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(&a.pay[wg]);
-        uint32_t v[3];
-        for (int j = 0; j < 3; ++j)
-            v[j] = wg == spec ? t_pay[j]
-                              : __hip_atomic_load(P + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        L->arp_ip = v[0];
-        L->arp_mac_lo = v[1];
-        L->arp_mac_hi = v[2];
-        L->arp_ok = 1;
-    }
-    if (lane == 1 && t_min[M_F6] != kNone && t_max[X_M6] != 0) {
-        const uint32_t wg = ((t_max[X_M6] - 1) / kTile) % gridDim.x;
-        const uint32_t* P = reinterpret_cast<const uint32_t*>(&a.pay[wg]);
-        uint32_t v[6];
-        for (int j = 0; j < 6; ++j)
-            v[j] = wg == spec ? t_pay[3 + j]
-                              : __hip_atomic_load(P + 3 + j, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        for (int j = 0; j < 4; ++j) L->ndp_ip[j] = v[j];
-        L->ndp_mac_lo = v[4];
-        L->ndp_mac_hi = v[5];
-        L->ndp_ok = 1;
-    }
     // re-arm the arrival tickets
     if (lane < kShards)
         __hip_atomic_store(&S->tickets.shard[lane][0], 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (lane == kShards)
         __hip_atomic_store(&S->tickets.top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// Residency census (one launch per kernel configuration, before its first batch): how many
+// workgroups of this kernel, with this much dynamic LDS, the chip really holds at once.  The
+// occupancy API can answer one workgroup per CU too many (MI355X_MICROARCH.md, "Residency and
+// cooperative launch"), and a persistent grid larger than what is resident runs its surplus
+// workgroups after the others, doubling the tail.  Each workgroup arrives on w[0] and waits (at
+// most ~30 us) for the whole grid; a workgroup that gives up records how many had arrived
+// (w[1], min), which is the resident count; nobody gives up when the whole grid is resident.
+// ------------------------------------------------------------------------------------------
+__device__ void census_probe(uint32_t* w, uint32_t grid) {
+    uint32_t v = __hip_atomic_fetch_add(&w[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (v < grid) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000) {
+            __hip_atomic_fetch_min(&w[1], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+        v = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -891,6 +866,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_last;    // this workgroup arrived last (set by wave 0)
 
+    if (a.census) {
+        if (threadIdx.x == 0) census_probe(a.census, gridDim.x);
+        return;
+    }
     if (kAblate & 64) return;
     STAMP(0);
     const int tid = threadIdx.x;
@@ -914,19 +893,47 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) d4[k] = g4[k];
         for (uint32_t k = tid; k < 4 * a.nrules_pad; k += kBlock) d6[k] = g6[k];
     }
+    // The starting L1 entries: the state after batch k - 2 (one scalar load) with batch k - 1's
+    // outcome folded in (its replicated minima / maxima, then at most two payload loads).
+    // DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4], ndp_mac_lo/hi, arp_ok, ndp_ok.
+    static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
+    const u32x16 lin = *as_const<u32x16>(a.l1_in);
+    uint4 pr = make_uint4(kNone, kNone, 0u, 0u);
+    if (lane < kReps) pr = a.acc_prev->l1r[lane];
+    const uint32_t pgrid = *as_const<uint32_t>(&a.acc_prev->grid);
     // small ARP indexes (<= 16 KB) into LDS after the rule-stats bins: a lookup is then an LDS
     // read, not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
     if (a.arp_lds)
         for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
-    // The starting L1 entries, as wave-uniform (scalar) loads that stay in flight while the
-    // first descriptors and frames load.  DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4],
-    // ndp_mac_lo/hi, arp_ok, ndp_ok.
-    static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
-    const u32x16 l1w = *as_const<u32x16>(&a.st->l1);
+    uint32_t L1[11];
+    if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
+#pragma unroll
+        for (int j = 0; j < 11; ++j) L1[j] = lin[j];
+    } else {
+        fold_l1(lin, wave_reduce<1>(pr.x), wave_reduce<1>(pr.y), wave_reduce<2>(pr.z),
+                wave_reduce<2>(pr.w), pgrid ? pgrid : 1u, a.pay_prev, L1);
+    }
+    if (blockIdx.x == 0) {
+        // workgroup 0: publish the folded state for batch k + 1, re-arm its accumulators
+        if (tid == 0) {
+            uint4* o = reinterpret_cast<uint4*>(a.l1_out);
+            o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
+            o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
+            o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
+            o[3] = make_uint4(0u, 0u, 0u, 0u);
+            a.acc_cur->grid = gridDim.x;
+        }
+        uint32_t* nc = &a.acc_next->cnt[0][0];
+        for (uint32_t k = tid; k < (uint32_t)(kReps * C_N); k += kBlock) nc[k] = 0u;
+        if (tid < kReps) {
+            a.acc_next->l1r[tid] = make_uint4(kNone, kNone, 0u, 0u);
+            a.acc_next->ctrl[tid] = kNone;
+        }
+    }
     __syncthreads();
-    const bool look4 = l1w[9] == 0u;    // the ARP entry disagrees with the table
-    const bool look6 = l1w[10] == 0u;   // the NDP entry disagrees with the table
+    const bool look4 = L1[9] == 0u;    // the ARP entry disagrees with the table
+    const bool look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
     STAMP(1);
 
     // Per-lane accumulators over this workgroup's tiles, reduced once at the end (not per tile):
@@ -1097,14 +1104,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             } else if (!r.v6) {
                 wrote1 = true;
                 hit = nhit;
-                cand = l1w[0] != 0 && r.d[0] == l1w[0];
+                cand = L1[0] != 0 && r.d[0] == L1[0];
                 fp4 = !cand && hit;
                 thit4 = hit;
             } else {
                 wrote1 = true;
                 hit = nhit;
-                cand = r.d[0] == l1w[3] && r.d[1] == l1w[4] && r.d[2] == l1w[5] &&
-                       r.d[3] == l1w[6];
+                cand = r.d[0] == L1[3] && r.d[1] == L1[4] && r.d[2] == L1[5] &&
+                       r.d[3] == L1[6];
                 fp6 = !cand && hit;
                 thit6 = hit;
             }
@@ -1234,7 +1241,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (wave == 0) {
     // ---- wave 0: flush the workgroup into the replicated accumulators ----
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
-    // so every accumulator kind goes out as ONE instruction, lane k carrying field k.
+    // so every accumulator kind goes out as ONE instruction, lane k carrying field k.  Nothing
+    // waits for them: the next launch reads them (kernel boundary), the host reads them after a
+    // synchronisation.
     DevState* S = a.st;
     const uint32_t rep = blockIdx.x % kReps;
     uint32_t cb = 0, x4 = 0, x6 = 0;
@@ -1245,26 +1254,33 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (s_wv[v][11] > x4) { x4 = s_wv[v][11]; w4 = v; }
         if (s_wv[v][12] > x6) { x6 = s_wv[v][12]; w6 = v; }
     }
-    const bool flag = (look4 || look6) && cb;
+    const bool look = look4 || look6;
+    const bool flag = look && cb;
     if (!(kAblate & 4)) {
-        if (lane < C_N) {
-            uint32_t cv = 0;
+        uint32_t cv = 0, tv = 0;   // lane c < C_N: counter c; lane j < 8: total j
 #pragma unroll
-            for (int v = 0; v < kWaves; ++v) cv += lane < 8 ? s_wv[v][lane] : 0u;
-            if (lane == C_CAND) cv = flag ? 1u : 0u;
-            if (cv) atomicAdd(&S->acc.cnt[rep][lane], cv);
+        for (int v = 0; v < kWaves; ++v) {
+            cv += lane < C_N ? s_wv[v][lane] : 0u;
+            tv += lane >= 1 && lane < 8 ? s_wv[v][lane - 1] : 0u;
         }
-        if (lane < M_N) {
-            // M_F4, M_F6, M_CTRL <- wave slots 8, 9, 10
-            uint32_t mv = kNone;
+        if (lane < C_N && cv) atomicAdd(&a.acc_cur->cnt[rep][lane], cv);
+        // cumulative totals in upe_counters_t order: pkts_in (the batch size, by workgroup 0),
+        // then C_PARSED .. C_ARP_REPLY
+        if (lane == 0 && blockIdx.x == 0) tv = a.n;
+        if (lane < 8 && tv) atomicAdd(&S->totals[rep][lane], (unsigned long long)tv);
+        // L1 outcome: first miss-then-hit (min) and last table hit (max) per family
+        uint32_t f4 = kNone, f6 = kNone, fc = kNone;
 #pragma unroll
-            for (int v = 0; v < kWaves; ++v) mv = min(mv, s_wv[v][8 + lane]);
-            if (mv != kNone) atomicMin(&S->acc.mins[rep][lane], mv);
+        for (int v = 0; v < kWaves; ++v) {
+            f4 = min(f4, s_wv[v][8]);
+            f6 = min(f6, s_wv[v][9]);
+            fc = min(fc, s_wv[v][10]);
         }
-        if (lane < X_N) {
-            const uint32_t xv = lane == X_M4 ? x4 : x6;
-            if (xv) atomicMax(&S->acc.maxs[rep][lane], xv);
-        }
+        uint32_t* r4 = reinterpret_cast<uint32_t*>(&a.acc_cur->l1r[rep]);
+        if ((lane == 0 && f4 != kNone) || (lane == 1 && f6 != kNone))
+            atomicMin(r4 + lane, lane == 0 ? f4 : f6);
+        if ((lane == 2 && x4) || (lane == 3 && x6)) atomicMax(r4 + lane, lane == 2 ? x4 : x6);
+        if (lane == 4 && fc != kNone) atomicMin(&a.acc_cur->ctrl[rep], fc);
         if (lds_stats && small_stats) {
             for (uint32_t k = lane; k < 2 * a.nrules_pad; k += 64) {
                 const uint32_t v = lds_hist[k];
@@ -1272,38 +1288,51 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
         }
     }
-    // the workgroup's last table hit per family (only the one holding the batch maximum is read)
+    // the workgroup's last table hit per family (the next launch reads the one the batch
+    // maximum points at)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(&a.pay[blockIdx.x]) + lane,
-                           s_pay[lane < 3 ? w4 : w6][lane], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (flag) {
-        // packets here may take the starting entry's answer: publish their verdicts and frames
-        // to the last workgroup (release: write back this XCD's L2)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
-    STAMP(5);
-    // every atomic and payload store of this workgroup is performed before the arrival ticket
-    __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    STAMP(6);
+        reinterpret_cast<uint32_t*>(&a.pay[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
     uint32_t last = 0;
-    if (lane == 0) {
-        const uint32_t nb = gridDim.x;
-        const uint32_t sh = blockIdx.x % kShards;
-        const uint32_t nsh = nb < (uint32_t)kShards ? nb : (uint32_t)kShards;
-        const uint32_t per = nb / kShards + (sh < nb % kShards ? 1u : 0u);
-        if (__hip_atomic_fetch_add(&S->tickets.shard[sh][0], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) == per - 1)
-            last = __hip_atomic_fetch_add(&S->tickets.top[0], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+    if (look && !(kAblate & 128)) {
+        // A starting entry disagrees with the table: packets of this batch aimed at it take the
+        // entry's MAC only if no earlier packet missed the entry and hit the table, which the
+        // last workgroup to arrive decides.  Arrival tickets carry whether anyone holds such
+        // packets (bits 16..), so that workgroup repairs only when there is something to repair.
+        if (flag) {
+            // publish this workgroup's verdicts and records / frames (release: write back this
+            // XCD's L2)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        }
+        STAMP(5);
+        // every atomic of this workgroup is performed before its arrival ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(6);
+        if (lane == 0) {
+            const uint32_t nb = gridDim.x;
+            const uint32_t sh = blockIdx.x % kShards;
+            const uint32_t nsh = nb < (uint32_t)kShards ? nb : (uint32_t)kShards;
+            const uint32_t per = nb / kShards + (sh < nb % kShards ? 1u : 0u);
+            const uint32_t mine = 1u | (flag ? 0x10000u : 0u);
+            const uint32_t os = __hip_atomic_fetch_add(&S->tickets.shard[sh][0], mine,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((os & 0xFFFFu) == per - 1) {
+                const uint32_t sc = (os >> 16) + (mine >> 16);
+                const uint32_t up = 1u | (sc ? 0x10000u : 0u);
+                const uint32_t ot = __hip_atomic_fetch_add(&S->tickets.top[0], up,
+                                                           __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                if ((ot & 0xFFFFu) == nsh - 1) last = 1u | ((((ot >> 16) + (up >> 16)) ? 1u : 0u) << 1);
+            }
+        }
     }
     if (lane == 0) s_last = last;
     STAMP(7);
     }   // wave 0
-    // the other waves wait here, so the last workgroup folds the batch with all its threads
+    if (!(look4 || look6)) return;
+    // the other waves wait here, so the last workgroup repairs with all its threads
     __syncthreads();
     if (!s_last) return;
-    batch_tail<kEmit>(a, tid, look4, look6);
+    batch_tail<kEmit>(a, tid, look4, look6, (s_last & 2u) != 0, L1);
     STAMP(8);
 }
 
@@ -1568,22 +1597,21 @@ struct upe_gpu_ctx {
     uint32_t arp_bits = 0, arp_seed = 0;
     uint4* ndp = nullptr;
     uint32_t ndp_bits = 0, ndp_seed = 0;
-    // state: one DevState allocation; the named members are device addresses inside it
+    // state: one DevState allocation (see "Sequential state between batches")
     DevState* st = nullptr;
-    DevL1* l1 = nullptr;
-    DevTotals* totals = nullptr;
-    BatchAcc* acc = nullptr;
-    Tickets* tickets = nullptr;
-    unsigned long long* acc_stats = nullptr;   // [kReps][2 * kSmallRules] (small tables)
+    uint64_t k = 0;                // launches so far: the next batch is batch k
+    uint32_t last_n = 0;           // the last batch's size (batch_info)
     unsigned long long* stats = nullptr;   // [cap][2]
+    TilePay* pay = nullptr;        // [2][paycap] per-workgroup last-hit payloads, by batch parity
+    uint32_t paycap = 0;           // largest grid
     // per-batch scratch
-    TilePay* pay = nullptr;        // [ntiles]
     uint32_t* cand_tile = nullptr; // [ntiles], zero between batches
     size_t tiles_alloc = 0;
+    // every launch and state upload is ordered after the previous one, whatever its stream
+    hipStream_t last_stream = nullptr;
+    hipEvent_t order_ev = nullptr;
     int cus = 256;
-    uint32_t resident = 0;         // persistent grid size for resident_lds bytes of dynamic LDS
-    size_t resident_lds = 0;
-    bool resident_tss = false;
+    std::map<uint64_t, uint32_t> resident;   // persistent grid per (lds, tss, emit) (census)
     int blocks_per_cu_override = 0;   // UPE_GPU_BLOCKS_PER_CU (diagnostic)
     uint32_t port_mac_lo = 0, port_mac_hi = 0, port_ip4 = 0;
     bool have_batch = false;
@@ -1686,13 +1714,10 @@ int publish(upe_gpu_ctx* c) {
 
 int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
     if (ntiles > c->tiles_alloc) {
-        if (c->pay) (void)hipFree(c->pay);
         if (c->cand_tile) (void)hipFree(c->cand_tile);
-        c->pay = nullptr;
         c->cand_tile = nullptr;
         c->tiles_alloc = 0;
         size_t want = ntiles + ntiles / 4 + 16;
-        HIP_TRY(hipMalloc(&c->pay, want * sizeof(TilePay)));
         HIP_TRY(hipMalloc(&c->cand_tile, want * sizeof(uint32_t)));
         HIP_TRY(hipMemset(c->cand_tile, 0, want * sizeof(uint32_t)));
         c->tiles_alloc = want;
@@ -1701,27 +1726,128 @@ int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
     return 0;
 }
 
+// Order work about to be queued on `s` after everything queued so far on the context's state
+// (the last launch, or a state upload), whatever stream that went to.
+int order_on(upe_gpu_ctx* c, hipStream_t s) {
+    if (c->last_stream && c->last_stream != s) {
+        HIP_TRY(hipEventRecord(c->order_ev, c->last_stream));
+        HIP_TRY(hipStreamWaitEvent(s, c->order_ev, 0));
+    }
+    c->last_stream = s;
+    return 0;
+}
+
+// The state slots of batch k (DevState comment).
+DevL1* l1_slot(upe_gpu_ctx* c, uint64_t k) { return &c->st->l1[k % 2]; }
+BatchAcc* acc_slot(upe_gpu_ctx* c, uint64_t k) { return &c->st->acc[k % 3]; }
+TilePay* pay_slot(upe_gpu_ctx* c, uint64_t k) { return c->pay + (size_t)(k % 2) * c->paycap; }
+
+// Does the L1 state the next batch starts from agree with the tables?  (After l1_sync.)
 int refresh(upe_gpu_ctx* c) {
-    hipLaunchKernelGGL(upe_refresh, dim3(1), dim3(64), 0, c->stream, c->l1, arp_index(c),
-                       ndp_index(c));
+    if (order_on(c, c->stream) != 0) return -1;
+    hipLaunchKernelGGL(upe_refresh, dim3(1), dim3(64), 0, c->stream, l1_slot(c, c->k),
+                       arp_index(c), ndp_index(c));
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-// Accumulators, small-table stats replicas and arrival tickets in their between-batch state
-// (every batch's last workgroup leaves them so).
-int arm_acc(upe_gpu_ctx* c) {
-    HIP_TRY(hipMemsetAsync(c->acc, 0, sizeof(BatchAcc), c->stream));
-    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(c->acc) + offsetof(BatchAcc, mins), 0xFF,
-                           sizeof(((BatchAcc*)nullptr)->mins), c->stream));
-    HIP_TRY(hipMemsetAsync(c->tickets, 0, sizeof(Tickets), c->stream));
-    HIP_TRY(hipMemsetAsync(c->acc_stats, 0,
-                           (size_t)kReps * kSmallRules * 2 * sizeof(unsigned long long), c->stream));
+// Fold the last batch's L1 outcome into l1[k % 2], the state the next batch starts from (and
+// clear it from that batch's accumulators, so the next launch does not fold it again).
+int l1_sync(upe_gpu_ctx* c) {
+    if (c->k == 0) return 0;
+    if (order_on(c, c->stream) != 0) return -1;
+    hipLaunchKernelGGL(upe_l1_sync, dim3(1), dim3(64), 0, c->stream, l1_slot(c, c->k),
+                       acc_slot(c, c->k + 2), pay_slot(c, c->k + 1));
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+// The between-batch state of a fresh context (a calloc'd worker_t): L1 all zero, accumulators
+// armed (nothing happened), tickets and totals zero.
+int arm_state(upe_gpu_ctx* c) {
+    if (order_on(c, c->stream) != 0) return -1;
+    static DevState init;   // zero, then the armed accumulator fields
+    for (auto& acc : init.acc) {
+        for (int r = 0; r < kReps; ++r) {
+            acc.l1r[r] = make_uint4(kNone, kNone, 0u, 0u);
+            acc.ctrl[r] = kNone;
+        }
+        acc.grid = 1;
+    }
+    HIP_TRY(hipMemcpyAsync(c->st, &init, offsetof(DevState, pay), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->k = 0;
+    c->last_n = 0;
     return 0;
 }
 
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+void launch_classify(bool tss, bool emit, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
+    if (tss && emit)
+        hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a);
+    else if (tss)
+        hipLaunchKernelGGL((upe_classify<true, false>), dim3(grid), dim3(kBlock), lds, s, a);
+    else if (emit)
+        hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
+}
+
+// The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
+// launch the first time the configuration is used (census_probe).  0 on error.
+uint32_t resident_grid(upe_gpu_ctx* c, bool tss, bool emit, size_t lds, hipStream_t s) {
+    const uint64_t key = (uint64_t)lds << 2 | (tss ? 2u : 0u) | (emit ? 1u : 0u);
+    auto it = c->resident.find(key);
+    if (it != c->resident.end()) return it->second;
+    int per_cu = 0;
+    hipError_t e;
+    if (tss && emit)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, true>, kBlock, lds);
+    else if (tss)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, false>, kBlock, lds);
+    else if (emit)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true>, kBlock, lds);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false>, kBlock, lds);
+    if (e != hipSuccess) {
+        fail(std::string("hipOccupancyMaxActiveBlocksPerMultiprocessor: ") + hipGetErrorString(e));
+        return 0;
+    }
+    if (per_cu < 1) per_cu = 1;
+    uint32_t grid = (uint32_t)per_cu * (uint32_t)c->cus;
+    if (c->blocks_per_cu_override > 0) {
+        grid = (uint32_t)c->blocks_per_cu_override * (uint32_t)c->cus;   // diagnostic
+    } else {
+        if (grid > c->paycap) grid = c->paycap;
+        Args a;
+        memset(&a, 0, sizeof a);
+        a.census = &c->st->census[0];
+        const uint32_t init[2] = {0u, kNone};
+        if (hipMemcpyAsync(a.census, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) {
+            fail("census upload failed");
+            return 0;
+        }
+        launch_classify(tss, emit, grid, lds, s, a);
+        uint32_t out[2] = {0u, 0u};
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(out, a.census, sizeof out, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            fail("census launch failed");
+            return 0;
+        }
+        if (out[1] != kNone && out[1] < grid) {
+            // round down to whole workgroups per CU
+            const uint32_t per = out[1] / (uint32_t)c->cus;
+            grid = (per ? per : 1u) * (uint32_t)c->cus;
+        }
+    }
+    if (grid > c->paycap) grid = c->paycap;
+    c->resident[key] = grid;
+    return grid;
+}
 
 }  // namespace
 
@@ -1756,13 +1882,10 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
     if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return bad(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming)) != hipSuccess)
+        return bad(e, "hipEventCreate");
     if ((e = hipMalloc(&c->st, sizeof(DevState))) != hipSuccess) return bad(e, "hipMalloc state");
     if ((e = hipMemset(c->st, 0, sizeof(DevState))) != hipSuccess) return bad(e, "hipMemset");
-    c->l1 = &c->st->l1;
-    c->totals = &c->st->totals;
-    c->acc = &c->st->acc;
-    c->tickets = &c->st->tickets;
-    c->acc_stats = &c->st->acc_stats[0][0];
     if ((e = hipMalloc(&c->stats, rule_capacity * 2 * sizeof(unsigned long long))) != hipSuccess)
         return bad(e, "hipMalloc stats");
     {
@@ -1772,15 +1895,19 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
             c->cus = cus;
         if (const char* v = getenv("UPE_GPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = atoi(v);
     }
-    if (arm_acc(c) != 0) {
+    // payload slots for the largest grid a launch uses (8 workgroups of 256 threads per CU)
+    c->paycap = 8u * (uint32_t)c->cus;
+    if ((e = hipMalloc(&c->pay, 2 * (size_t)c->paycap * sizeof(TilePay))) != hipSuccess)
+        return bad(e, "hipMalloc payloads");
+    if ((e = hipMemset(c->pay, 0, 2 * (size_t)c->paycap * sizeof(TilePay))) != hipSuccess)
+        return bad(e, "hipMemset");
+    if (arm_state(c) != 0) {
         std::string m = g_err;
         upe_gpu_close(c);
         g_err = m;
         return nullptr;
     }
-    if ((e = hipMemsetAsync(c->l1, 0, sizeof(DevL1), c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->totals, 0, sizeof(DevTotals), c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->stats, 0, rule_capacity * 2 * sizeof(unsigned long long),
+    if ((e = hipMemsetAsync(c->stats, 0, rule_capacity * 2 * sizeof(unsigned long long),
                             c->stream)) != hipSuccess)
         return bad(e, "hipMemsetAsync");
     // An empty rule table: one padding block of never-matching rules.
@@ -1810,6 +1937,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     for (auto& sl : c->hs) {
         for (void* b : {(void*)sl.frames, (void*)sl.desc, (void*)sl.verdict})
             if (b) (void)hipFree(b);
@@ -1837,6 +1965,14 @@ int read_stats_idx(upe_gpu_ctx* c, std::vector<unsigned long long>& idx) {
     idx.assign(E, 0);
     for (size_t r = 0; r < (size_t)kStatReps; ++r)
         for (size_t e = 0; e < E; ++e) idx[e] += all[r * E + e];
+    if (E <= 2 * (size_t)kSmallRules) {
+        // small tables: the classify kernel's replicated per-sorted-index totals
+        std::vector<unsigned long long> sm((size_t)kReps * 2 * kSmallRules);
+        HIP_TRY(hipMemcpy(sm.data(), &c->st->acc_stats[0][0], sm.size() * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost));
+        for (size_t r = 0; r < (size_t)kReps; ++r)
+            for (size_t e = 0; e < E; ++e) idx[e] += sm[r * 2 * kSmallRules + e];
+    }
     return 0;
 }
 
@@ -1856,6 +1992,7 @@ int fold_stats_idx(upe_gpu_ctx* c) {
     HIP_TRY(hipMemcpy(c->stats, st.data(), st.size() * sizeof(unsigned long long),
                       hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(c->stats_idx, 0, E * kStatReps * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats)));
     return 0;
 }
 }  // namespace
@@ -2030,7 +2167,9 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         if (v6w) a.m1 |= kRuleV6Words;   // IPv6 keys must test this rule's rv6 words
         info[i] = make_int2(r.action.type, (int)r.rule_id);
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));   // previous batches may still read the table
+    // previous batches may still read the table, on whichever stream they went
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     if (fold_stats_idx(c) != 0) return -1;
     if (pad > c->rules_alloc) {
         if (c->rv4) (void)hipFree(c->rv4);
@@ -2156,6 +2295,9 @@ int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_
     }
     if (a.empty()) a.push_back(make_uint4(0, 0, 0, 0));   // keep a valid allocation
     if (b.empty()) b.resize(2, make_uint4(0, 0, 0, 0));
+    // the last batch's L1 outcome into the starting state before the tables change
+    if (c->st && l1_sync(c) != 0) return -1;
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->arp) (void)hipFree(c->arp);
     if (c->ndp) (void)hipFree(c->ndp);
@@ -2168,7 +2310,7 @@ int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_
     c->arp_seed = aseed;
     c->ndp_bits = nbits;
     c->ndp_seed = nseed;
-    if (c->l1 && refresh(c) != 0) return -1;   // does the L1 state agree with the new tables?
+    if (c->st && refresh(c) != 0) return -1;   // does the L1 state agree with the new tables?
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -2192,7 +2334,9 @@ int upe_gpu_set_l1(upe_gpu_ctx_t* c, const upe_l1_state_t* l1) {
     for (int j = 0; j < 4; ++j) d.ndp_ip[j] = le32(l1->last_ndp_ip + 4 * j);
     d.ndp_mac_lo = mac_lo(l1->last_ndp_mac);
     d.ndp_mac_hi = mac_hi(l1->last_ndp_mac);
-    HIP_TRY(hipMemcpyAsync(c->l1, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+    // the pending batch's outcome is replaced, not folded in later: fold (clears it), overwrite
+    if (l1_sync(c) != 0) return -1;
+    HIP_TRY(hipMemcpyAsync(l1_slot(c, c->k), &d, sizeof d, hipMemcpyHostToDevice, c->stream));
     if (refresh(c) != 0) return -1;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
@@ -2201,9 +2345,10 @@ int upe_gpu_set_l1(upe_gpu_ctx_t* c, const upe_l1_state_t* l1) {
 int upe_gpu_get_l1(upe_gpu_ctx_t* c, upe_l1_state_t* l1) {
     if (!c || !l1) return fail("null argument");
     HIP_TRY(hipSetDevice(c->device));
+    if (l1_sync(c) != 0) return -1;
     HIP_TRY(hipDeviceSynchronize());
     DevL1 d;
-    HIP_TRY(hipMemcpy(&d, c->l1, sizeof d, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&d, l1_slot(c, c->k), sizeof d, hipMemcpyDeviceToHost));
     memset(l1, 0, sizeof *l1);
     l1->last_arp_ip = d.arp_ip;
     memcpy(l1->last_arp_mac, &d.arp_mac_lo, 4);
@@ -2230,14 +2375,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     hipStream_t s = pick(c, stream);
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     if (ensure_scratch(c, ntiles ? ntiles : 1) != 0) return -1;
-    if (s != c->stream) {
-        // the context's own uploads (tables, L1) were queued on its stream: order after them
-        hipEvent_t dep;
-        HIP_TRY(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(dep, c->stream));
-        HIP_TRY(hipStreamWaitEvent(s, dep, 0));
-        HIP_TRY(hipEventDestroy(dep));
-    }
+    // after the context's previous launch and its own uploads (tables, L1), on whichever stream
+    // they went: a batch starts from the state the one before it left
+    if (order_on(c, s) != 0) return -1;
     // timing sample: an event pair around `timing_span` consecutive calls, opened on every
     // timing_every-th call (samples never overlap)
     const bool open = c->timing && c->t_left == 0 && (c->timing_calls % c->timing_every) == 0;
@@ -2252,6 +2392,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         c->t_left = c->timing_span;
     }
     Args a;
+    memset(&a, 0, sizeof a);   // every field a launch does not set stays null / zero
     a.frames = d_frames;
     a.desc = d_desc;
     a.verdict = d_verdict;
@@ -2276,7 +2417,13 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
     a.tss = c->tss ? 1u : 0u;
-    a.pay = c->pay;
+    a.pay = pay_slot(c, c->k);
+    a.pay_prev = pay_slot(c, c->k + 1);
+    a.l1_in = l1_slot(c, c->k);
+    a.l1_out = l1_slot(c, c->k + 1);
+    a.acc_cur = acc_slot(c, c->k);
+    a.acc_prev = acc_slot(c, c->k + 2);
+    a.acc_next = acc_slot(c, c->k + 1);
     a.cand_tile = c->cand_tile;
     a.stats = c->stats;
     a.stats_idx = c->stats_idx;
@@ -2303,25 +2450,10 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.arp_lds = (arp_slots && arp_slots <= kArpLdsSlots && hist <= 8192) ? arp_slots : 0u;
     const size_t lds = hist + (size_t)a.arp_lds * sizeof(uint4);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
-    if (c->resident_lds != lds || c->resident == 0 || c->resident_tss != c->tss) {
-        c->resident_tss = c->tss;
-        int per_cu = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, c->tss ? upe_classify<true, false> : upe_classify<false, false>, kBlock, lds));
-        if (per_cu < 1) per_cu = 1;
-        if (c->blocks_per_cu_override > 0) per_cu = c->blocks_per_cu_override;
-        c->resident = (uint32_t)per_cu * (uint32_t)c->cus;
-        c->resident_lds = lds;
-    }
-    const uint32_t grid = ntiles == 0 ? 1u : ntiles < c->resident ? ntiles : c->resident;
-    if (c->tss && emit)
-        hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a);
-    else if (c->tss)
-        hipLaunchKernelGGL((upe_classify<true, false>), dim3(grid), dim3(kBlock), lds, s, a);
-    else if (emit)
-        hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a);
-    else
-        hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
+    const uint32_t grid_cap = resident_grid(c, c->tss, emit, lds, s);
+    if (grid_cap == 0) return -1;
+    const uint32_t grid = ntiles == 0 ? 1u : ntiles < grid_cap ? ntiles : grid_cap;
+    launch_classify(c->tss, emit, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
@@ -2351,6 +2483,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         c->ev_used += 2;
         c->timing_launches += c->timing_span;
     }
+    ++c->k;
+    c->last_n = (uint32_t)n;
     c->have_batch = true;
     return 0;
 }
@@ -2709,17 +2843,20 @@ int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
     if (!c || !info) return fail("null argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    DevTotals t;
-    HIP_TRY(hipMemcpy(&t, c->totals, sizeof t, hipMemcpyDeviceToHost));
     memset(info, 0, sizeof *info);
-    if (!c->have_batch) {
-        info->first_ctrl = ~0ull;
-        return 0;
-    }
+    info->first_ctrl = ~0ull;
+    if (!c->have_batch || c->k == 0) return 0;
+    BatchAcc b;   // the last batch's accumulators
+    HIP_TRY(hipMemcpy(&b, acc_slot(c, c->k + 2), sizeof b, hipMemcpyDeviceToHost));
     uint64_t* dst = &info->counters.pkts_in;
-    for (int j = 0; j < 8; ++j) dst[j] = t.batch[j];
-    info->n_ctrl = t.n_ctrl;
-    info->first_ctrl = t.first_ctrl;
+    dst[0] = c->last_n;
+    uint32_t first = kNone;
+    for (int r = 0; r < kReps; ++r) {
+        for (int j = 0; j < 7; ++j) dst[1 + j] += b.cnt[r][j];
+        info->n_ctrl += b.cnt[r][C_CTRL];
+        first = std::min(first, b.ctrl[r]);
+    }
+    if (first != kNone) info->first_ctrl = first;
     return 0;
 }
 
@@ -2729,10 +2866,13 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
     if (counters) {
-        DevTotals t;
-        HIP_TRY(hipMemcpy(&t, c->totals, sizeof t, hipMemcpyDeviceToHost));
+        unsigned long long t[kReps][8];
+        HIP_TRY(hipMemcpy(t, &c->st->totals[0][0], sizeof t, hipMemcpyDeviceToHost));
         uint64_t* dst = &counters->pkts_in;
-        for (int j = 0; j < 8; ++j) dst[j] = t.cnt[j];
+        for (int j = 0; j < 8; ++j) {
+            dst[j] = 0;
+            for (int r = 0; r < kReps; ++r) dst[j] += t[r][j];
+        }
     }
     if (rule_stats) {
         const size_t k = capacity < c->cap ? capacity : c->cap;
@@ -2756,7 +2896,9 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
 int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
     if (!c) return fail("null context");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->totals, 0, sizeof(DevTotals), c->stream));
+    if (order_on(c, c->stream) != 0) return -1;
+    HIP_TRY(hipMemsetAsync(&c->st->totals[0][0], 0, sizeof(c->st->totals), c->stream));
+    HIP_TRY(hipMemsetAsync(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats), c->stream));
     HIP_TRY(hipMemsetAsync(c->stats, 0, c->cap * 2 * sizeof(unsigned long long), c->stream));
     if (c->stats_idx)
         HIP_TRY(hipMemsetAsync(c->stats_idx, 0,
