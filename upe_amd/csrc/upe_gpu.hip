@@ -72,9 +72,9 @@ constexpr int kBlock = UPE_BLOCK;      // threads per workgroup = packets per ti
 constexpr int kWaves = kBlock / 64;
 constexpr int kTile = kBlock;
 #ifndef UPE_WAVES_PER_SIMD
-#define UPE_WAVES_PER_SIMD 5
+#define UPE_WAVES_PER_SIMD 4
 #endif
-constexpr int kWavesPerSimd = UPE_WAVES_PER_SIMD;   // 8 -> VGPR budget 64
+constexpr int kWavesPerSimd = UPE_WAVES_PER_SIMD;   // 4 -> VGPR budget 128, 8 -> 64
 constexpr int kUnroll = 4;             // rules per early-exit check (rule table padding unit)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 #ifndef UPE_LDS_STATS_MAX
@@ -88,15 +88,12 @@ constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (s
 constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;   // ARP indexes up to 16 KB are staged in LDS
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
-constexpr int kShards = 8;             // arrival-ticket shards
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
 // 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 128 no arrival
 // ticket and no last-workgroup repair, 256 no fold of the previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
-// s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt not waited (gfx9 encoding)
-constexpr int kWaitVm0 = 0x0F70;
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
 // rv4[i]: header + first address word, used for every packet:
@@ -139,16 +136,20 @@ struct DevL1 {
 //   acc[k % 3]      this batch's accumulators, pay[k % 2] its payloads (written)
 //   acc[(k + 1) % 3] re-armed by workgroup 0 for batch k + 1
 // Host calls that read or replace the L1 state first fold the pending batch the same way
-// (upe_l1_sync).  Counters go straight into replicated cumulative totals, rule_stats into
-// replicated per-sorted-index totals; the host sums replicas when it reads them.
+// (upe_l1_sync).  Batch k's counters are folded into the cumulative totals by batch k + 1
+// (workgroups 0..7, one counter each); rule_stats go straight into replicated per-sorted-index
+// totals, which the host sums when it reads them.  No workgroup ever waits for another.
 enum { C_PARSED, C_MATCHED, C_FWD, C_DROPPED, C_CONSUMED, C_ARP_LEARN, C_ARP_REPLY, C_CTRL, C_N };
+// l1r words, all combined with atomicMax (minima stored as kNone - x, so "none" is 0)
+enum { R_F4, R_F6, R_M4, R_M6, R_CTRL, R_N = 8 };
 struct __attribute__((aligned(128))) BatchAcc {
     uint32_t cnt[kReps][C_N];   // this batch's counters
-    uint4 l1r[kReps];           // x, y: first miss-then-hit index v4 / v6 (min, kNone = none);
-                                // z, w: last table hit v4 / v6 (max of index + 1, 0 = none)
-    uint32_t ctrl[kReps];       // first control packet (min)
+    uint32_t l1r[kReps][R_N];   // R_F4 / R_F6: kNone - first miss-then-hit index v4 / v6;
+                                // R_M4 / R_M6: last table hit v4 / v6 (index + 1, 0 = none);
+                                // R_CTRL: kNone - first control packet
     uint32_t grid;              // the batch's grid (which workgroup holds a payload)
-    uint32_t pad[31];
+    uint32_t n;                 // the batch's size
+    uint32_t pad[30];
 };
 // Payload of a workgroup's last table hit per family; the next batch reads the one the batch
 // maximum points at.
@@ -158,24 +159,25 @@ struct __attribute__((aligned(64))) TilePay {
     uint32_t pad[7];
 };
 constexpr int kPayWords = 9;
-// Arrival tickets: shard s counts the workgroups b with b % kShards == s (one 128-byte line
-// each); a shard's last arrival bumps `top`, and the workgroup that completes `top` is last.
-struct Tickets {
-    uint32_t shard[kShards][32];
-    uint32_t top[32];
-};
+// Look-back flags (one word per 64-packet chunk: a wave's share of a tile), written only while
+// a starting L1 entry disagrees with the table: launch tag << 6 | bits.  A packet the starting
+// entry may answer needs to know whether any earlier packet of its family missed the entry and
+// hit the table; its wave looks back over the earlier chunks' flags (decoupled look-back).
+enum { LB_FP4 = 1, LB_FP6 = 2, LB_KNOWN4 = 4, LB_INCL4 = 8, LB_KNOWN6 = 16, LB_INCL6 = 32 };
+constexpr uint32_t kLbTagMod = 0x3FFFFFFu;   // tags 1 .. kLbTagMod
 
 // Everything a batch reads or writes besides the packets and the tables, in one device
 // allocation.
 struct DevState {
     DevL1 l1[2];
     BatchAcc acc[3];
-    Tickets tickets;
-    unsigned long long totals[kReps][8];                    // cumulative, upe_counters_t order
+    unsigned long long totals[8];                           // cumulative, upe_counters_t order
+    uint32_t lb_timeout;                                    // a look-back gave up (grid not resident)
+    uint32_t pad0[15];
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
     uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
-    uint32_t* cand_tile;             // [ntiles], zero between batches
+    uint32_t* lb;                    // [ntiles * kWaves] look-back flags
     unsigned long long* stats;       // [cap][2] worker rule_stats (mid-size and large tables)
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2] totals per sorted index
 };
@@ -226,7 +228,6 @@ struct Args {
     uint32_t ng4, ng6, tss;
     // the context's arrays, passed by value so that no kernel waits on a pointer load
     TilePay* pay;                    // [grid]
-    uint32_t* cand_tile;             // [ntiles]
     unsigned long long* stats;       // [cap][2]
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
@@ -241,6 +242,8 @@ struct Args {
     BatchAcc* acc_next;
     const TilePay* pay_prev;
     uint32_t* census;                // non-null: a residency census launch (census_probe) only
+    uint32_t* lb;                    // look-back flags [ntiles * kWaves]
+    uint32_t lb_tag;                 // this launch's flag tag
 };
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
@@ -445,15 +448,15 @@ __device__ __forceinline__ void fold_l1(const u32x16& in, uint32_t f4, uint32_t 
 // acc's L1 fields back to "nothing happened", so the next launch's own fold is the identity.
 __global__ void upe_l1_sync(DevL1* l1, BatchAcc* acc, const TilePay* pay) {
     const int lane = threadIdx.x;
-    uint4 pr = make_uint4(kNone, kNone, 0u, 0u);
-    if (lane < kReps) pr = acc->l1r[lane];
-    const uint32_t f4 = wave_reduce<1>(pr.x), f6 = wave_reduce<1>(pr.y);
+    uint4 pr = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < kReps) pr = *reinterpret_cast<const uint4*>(&acc->l1r[lane][0]);
+    const uint32_t f4 = kNone - wave_reduce<2>(pr.x), f6 = kNone - wave_reduce<2>(pr.y);
     const uint32_t m4 = wave_reduce<2>(pr.z), m6 = wave_reduce<2>(pr.w);
     const u32x16 in = *as_const<u32x16>(l1);
     uint32_t L[11];
     fold_l1(in, f4, f6, m4, m6, acc->grid ? acc->grid : 1u, pay, L);
     __syncthreads();
-    if (lane < kReps) acc->l1r[lane] = make_uint4(kNone, kNone, 0u, 0u);
+    if (lane < kReps) *reinterpret_cast<uint4*>(&acc->l1r[lane][0]) = make_uint4(0u, 0u, 0u, 0u);
     if (lane == 0) {
         uint32_t* w = reinterpret_cast<uint32_t*>(l1);
 #pragma unroll
@@ -755,76 +758,55 @@ __device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len,
 }
 
 // ------------------------------------------------------------------------------------------
-// The batch's last workgroup, when a starting L1 entry disagreed with the table (every other
-// workgroup has arrived): packets whose destination is that entry, before the batch's first
-// miss-then-hit packet of their family, took the entry's MAC in the reference
-// (src/worker.c:186-188, 218-220); their workgroups flagged the tiles and released their
-// stores.  anycand: some workgroup flagged a tile.  L1: the starting state (DevL1 words).
-// Re-arms the tickets.
+// Decoupled look-back (only while a starting L1 entry disagrees with the table).  A packet whose
+// destination is the starting entry took the entry's MAC in the reference (src/worker.c:186-188,
+// 218-220) iff no earlier packet of its family missed the entry and hit the table.  Every chunk
+// (a wave's 64 packets of a tile) publishes whether it holds such a packet; a wave holding
+// candidates reads the flags of the chunks before it, nearest first, until one holds such a
+// packet or one already knows the answer for everything up to it (LB_KNOWN*), waiting for any
+// chunk that has not published yet.  Chunks only ever wait for lower chunks, and every chunk
+// of the grid is resident (census), so the wait ends; a give-up after ~20 ms (which a resident
+// grid never reaches) is reported through DevState::lb_timeout.  Returns, for the families in
+// `need` (bit 0 v4, bit 1 v6), whether an earlier chunk holds a miss-then-hit packet.
 // ------------------------------------------------------------------------------------------
-template <bool kEmit>
-__device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, bool look6,
-                                           bool anycand, const uint32_t (&L1)[11]) {
-    DevState* S = a.st;
-    const int lane = tid & 63;
-    if (tid >= 64) return;   // wave 0 does it
-    if (anycand) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        // the batch's first miss-then-hit per family (every workgroup's atomics were performed
-        // before its ticket)
-        uint32_t x = kNone, y = kNone;
-        if (lane < kReps) {
-            const uint32_t* r = reinterpret_cast<const uint32_t*>(&a.acc_cur->l1r[lane]);
-            x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            y = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ uint32_t lookback(uint32_t* lb, uint32_t chunk, uint32_t tag, uint32_t need, int lane,
+                             uint32_t* timeout) {
+    uint32_t got = 0;
+    int64_t base = chunk;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (need && base > 0) {
+        const int64_t j = base - 64 + lane;
+        uint32_t f = 0;
+        bool ready = j < 0;
+        for (;;) {
+            if (!ready) {
+                f = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ready = (f >> 6) == tag;
+            }
+            if (__all(ready)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000u) {
+                if (lane == 0)
+                    __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return got;
+            }
+            __builtin_amdgcn_s_sleep(2);
         }
-        const uint32_t f[2] = {wave_reduce<1>(x), wave_reduce<1>(y)};
-        const uint32_t lo[2] = {L1[1], L1[7]};
-        const uint32_t hi[2] = {L1[2], L1[8]};
-        // nothing at or after the later of the two first-hit indexes needs the start entry
-        const uint32_t fmax = max(look4 ? f[0] : 0u, look6 ? f[1] : 0u);
-        const uint32_t tend = fmax == kNone ? a.ntiles : min(a.ntiles, fmax / kTile + 1);
-        for (uint32_t base = 0; base < tend; base += 64) {
-            const uint32_t t = base + (uint32_t)lane;
-            // flags were set with device atomics: read and re-arm them the same way
-            const uint32_t cbt = t < tend ? __hip_atomic_exchange(&a.cand_tile[t], 0u,
-                                                                  __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT)
-                                          : 0u;
-            unsigned long long pend = __ballot(cbt != 0);
-            while (pend) {
-                const int l = __ffsll((long long)pend) - 1;
-                pend &= pend - 1;
-                const uint32_t tt = base + (uint32_t)l;
-                const uint32_t fam_ok = (uint32_t)__shfl((int)cbt, l, 64);
-                for (uint32_t q = 0; q < (uint32_t)kTile; q += 64) {
-                    const uint32_t i = tt * kTile + q + (uint32_t)lane;
-                    if (i >= a.n) continue;
-                    const uint32_t v = a.verdict[i];
-                    if ((v & 0xFu) != UPE_V_FWD || !(v & UPE_VF_L1_INIT)) continue;
-                    uint8_t* p = a.frames + (a.desc[i] >> 16);
-                    const int fam = (p[12] == 0x86 && p[13] == 0xDD) ? 1 : 0;
-                    if (!((fam_ok >> fam) & 1u) || i >= f[fam]) continue;
-                    // emit mode: the packet's record holds the rewritten bytes 0..11
-                    uint32_t* w = kEmit ? reinterpret_cast<uint32_t*>(a.hdr + i)
-                                        : reinterpret_cast<uint32_t*>(p);
-                    w[0] = lo[fam];
-                    w[1] = hi[fam] | (a.port_mac_lo << 16);
-                    w[2] = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
-                    a.verdict[i] = v | UPE_VF_NEIGH_HIT;
-                }
+#pragma unroll
+        for (int F = 0; F < 2; ++F) {
+            const uint32_t fb = F ? LB_FP6 : LB_FP4;
+            const uint32_t kb = F ? LB_KNOWN6 : LB_KNOWN4, ib = F ? LB_INCL6 : LB_INCL4;
+            if (!(need & fb)) continue;
+            const unsigned long long info = __ballot(j >= 0 && (f & (fb | kb)));
+            if (info) {
+                const int hl = 63 - __builtin_clzll(info);   // the nearest chunk that knows
+                const uint32_t fh = (uint32_t)__shfl((int)f, hl, 64);
+                if (fh & (fb | ib)) got |= fb;
+                need &= ~fb;
             }
         }
-        // flagged tiles past tend keep their flag: clear them too
-        for (uint32_t t = tend + (uint32_t)lane; t < a.ntiles; t += 64)
-            __hip_atomic_store(&a.cand_tile[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base -= 64;
     }
-    // re-arm the arrival tickets
-    if (lane < kShards)
-        __hip_atomic_store(&S->tickets.shard[lane][0], 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == kShards)
-        __hip_atomic_store(&S->tickets.top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return got;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -833,14 +815,18 @@ __device__ __forceinline__ void batch_tail(const Args& a, int tid, bool look4, b
 // occupancy API can answer one workgroup per CU too many (MI355X_MICROARCH.md, "Residency and
 // cooperative launch"), and a persistent grid larger than what is resident runs its surplus
 // workgroups after the others, doubling the tail.  Each workgroup arrives on w[0] and waits (at
-// most ~30 us) for the whole grid; a workgroup that gives up records how many had arrived
-// (w[1], min), which is the resident count; nobody gives up when the whole grid is resident.
+// most ~60 us) for the whole grid; a workgroup that gives up records how many had arrived
+// when it gave up (w[1], min).  Resident workgroups all arrive within a few microseconds of
+// the first one and give up together, seeing every resident arrival and no other (the rest
+// can only start once a resident one has exited); nobody gives up when the whole grid is
+// resident.
 // ------------------------------------------------------------------------------------------
 __device__ void census_probe(uint32_t* w, uint32_t grid) {
     uint32_t v = __hip_atomic_fetch_add(&w[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
     while (v < grid) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 6000) {
+            v = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_min(&w[1], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
@@ -858,13 +844,12 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 template <bool kTssMode, bool kEmit>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
-    // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6, cand bits
-    __shared__ uint32_t s_wv[kWaves][14];
+    // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
+    __shared__ uint32_t s_wv[kWaves][13];
     __shared__ uint32_t s_pay[kWaves][kPayWords];
     __shared__ uint32_t s_lpay[kBlock][kPayWords];   // each lane's latest table hit
     __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
-    __shared__ uint32_t s_last;    // this workgroup arrived last (set by wave 0)
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.census, gridDim.x);
@@ -898,43 +883,34 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4], ndp_mac_lo/hi, arp_ok, ndp_ok.
     static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
     const u32x16 lin = *as_const<u32x16>(a.l1_in);
-    uint4 pr = make_uint4(kNone, kNone, 0u, 0u);
-    if (lane < kReps) pr = a.acc_prev->l1r[lane];
+    uint4 pr = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < kReps) pr = *reinterpret_cast<const uint4*>(&a.acc_prev->l1r[lane][0]);
     const uint32_t pgrid = *as_const<uint32_t>(&a.acc_prev->grid);
     // small ARP indexes (<= 16 KB) into LDS after the rule-stats bins: a lookup is then an LDS
     // read, not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
     if (a.arp_lds)
         for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
-    uint32_t L1[11];
-    if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
-#pragma unroll
-        for (int j = 0; j < 11; ++j) L1[j] = lin[j];
-    } else {
-        fold_l1(lin, wave_reduce<1>(pr.x), wave_reduce<1>(pr.y), wave_reduce<2>(pr.z),
-                wave_reduce<2>(pr.w), pgrid ? pgrid : 1u, a.pay_prev, L1);
-    }
-    if (blockIdx.x == 0) {
-        // workgroup 0: publish the folded state for batch k + 1, re-arm its accumulators
-        if (tid == 0) {
-            uint4* o = reinterpret_cast<uint4*>(a.l1_out);
-            o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
-            o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
-            o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
-            o[3] = make_uint4(0u, 0u, 0u, 0u);
-            a.acc_cur->grid = gridDim.x;
-        }
-        uint32_t* nc = &a.acc_next->cnt[0][0];
-        for (uint32_t k = tid; k < (uint32_t)(kReps * C_N); k += kBlock) nc[k] = 0u;
-        if (tid < kReps) {
-            a.acc_next->l1r[tid] = make_uint4(kNone, kNone, 0u, 0u);
-            a.acc_next->ctrl[tid] = kNone;
-        }
-    }
     __syncthreads();
-    const bool look4 = L1[9] == 0u;    // the ARP entry disagrees with the table
-    const bool look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
     STAMP(1);
+    // The fold itself waits on those loads (and then on at most two payload loads), so it runs
+    // after the first tile's frame loads are issued (or after the loop if there is no tile),
+    // off the path to the first frames.
+    uint32_t L1[11];
+    bool look4 = false, look6 = false, folded = false;
+    auto fold_start = [&]() {
+        if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
+#pragma unroll
+            for (int j = 0; j < 11; ++j) L1[j] = lin[j];
+        } else {
+            fold_l1(lin, kNone - wave_reduce<2>(pr.x), kNone - wave_reduce<2>(pr.y),
+                    wave_reduce<2>(pr.z), wave_reduce<2>(pr.w), pgrid ? pgrid : 1u, a.pay_prev,
+                    L1);
+        }
+        look4 = L1[9] == 0u;    // the ARP entry disagrees with the table
+        look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
+        folded = true;
+    };
 
     // Per-lane accumulators over this workgroup's tiles, reduced once at the end (not per tile):
     // counters as 16-bit pairs (a lane sees at most one packet per tile, and a workgroup takes
@@ -942,7 +918,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // min / max; each lane's latest table hit is kept in LDS (tiles ascend, so it is the
     // lane's last one).
     uint32_t c01 = 0, c23 = 0, c45 = 0, c67 = 0;
-    uint32_t lf4 = kNone, lf6 = kNone, lfc = kNone, lm4 = 0, lm6 = 0, wcb = 0;
+    uint32_t lf4 = kNone, lf6 = kNone, lfc = kNone, lm4 = 0, lm6 = 0;
     // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
     // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
     // workgroup, at the very end of its life, not once per tile.
@@ -977,6 +953,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             dsc_next = 0;
             if (nt < a.ntiles && nt * kTile + (uint32_t)tid < a.n) dsc_next = a.desc[nt * kTile + tid];
         }
+        if (!folded) fold_start();
 
         if (tile == blockIdx.x) STAMP_VM(2);
         // ---- fast path: option-less IPv4 / IPv6 ----
@@ -1117,6 +1094,42 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
             if (cand) flags |= UPE_VF_L1_INIT;
         }
+        if (look4 || look6) {
+            // The starting entry disagrees with the table: publish this chunk's miss-then-hit
+            // packets, and give the packets aimed at the entry the entry's MAC unless an earlier
+            // packet of their family missed it and hit the table (lookback).
+            const uint32_t chunk = tile * kWaves + (uint32_t)wave;
+            const unsigned long long b4 = __ballot(fp4), b6 = __ballot(fp6);
+            const uint32_t fpb = (b4 ? (uint32_t)LB_FP4 : 0u) | (b6 ? (uint32_t)LB_FP6 : 0u);
+            const uint32_t tag = a.lb_tag << 6;
+            if (lane == 0)
+                __hip_atomic_store(&a.lb[chunk], tag | fpb, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const bool c4 = cand && !r.v6 && look4, c6 = cand && r.v6 && look6;
+            const uint32_t need = (__ballot(c4) ? (uint32_t)LB_FP4 : 0u) |
+                                  (__ballot(c6) ? (uint32_t)LB_FP6 : 0u);
+            if (need) {
+                const uint32_t before = lookback(a.lb, chunk, a.lb_tag, need, lane,
+                                                 &a.st->lb_timeout);
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const bool prior4 = (before & LB_FP4) || (b4 & lt);
+                const bool prior6 = (before & LB_FP6) || (b6 & lt);
+                if ((c4 && !prior4) || (c6 && !prior6)) {
+                    hit = true;
+                    mlo = r.v6 ? L1[7] : L1[1];
+                    mhi = r.v6 ? L1[8] : L1[2];
+                }
+                // what this chunk now knows about everything up to it
+                uint32_t kn = 0;
+                if (need & LB_FP4)
+                    kn |= LB_KNOWN4 | (((before & LB_FP4) || b4) ? (uint32_t)LB_INCL4 : 0u);
+                if (need & LB_FP6)
+                    kn |= LB_KNOWN6 | (((before & LB_FP6) || b6) ? (uint32_t)LB_INCL6 : 0u);
+                if (lane == 0)
+                    __hip_atomic_store(&a.lb[chunk], tag | fpb | kn, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         if (hit) flags |= UPE_VF_NEIGH_HIT;
 
         // ---- write back ----
@@ -1178,19 +1191,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             s_lpay[tid][3] = r.d[0]; s_lpay[tid][4] = r.d[1]; s_lpay[tid][5] = r.d[2];
             s_lpay[tid][6] = r.d[3]; s_lpay[tid][7] = mlo; s_lpay[tid][8] = mhi;
         }
-        if (look4 || look6) {
-            // packets the starting entry answers if nothing before them missed it and hit the
-            // table: flag the tile, and drain this wave's stores so the release below covers them
-            const uint32_t cbits = (__ballot(cand && !r.v6 && look4) ? 1u : 0u) |
-                                   (__ballot(cand && r.v6 && look6) ? 2u : 0u);
-            if (cbits) {
-                if (lane == 0) atomicOr(&a.cand_tile[tile], cbits);
-                wcb = __builtin_amdgcn_readfirstlane(wcb | cbits);
-                __builtin_amdgcn_s_waitcnt(kWaitVm0);
-            }
-        }
     }
     STAMP(4);
+    if (!folded) fold_start();
     // ---- reduce the per-lane accumulators: DPP rotations inside each 16-lane row, then the four
     // row results through scalar registers; then across the workgroup's waves in LDS ----
     {
@@ -1212,7 +1215,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (lane == 0) {
 #pragma unroll
             for (int c = 0; c < 13; ++c) s_wv[w][c] = v[c];
-            s_wv[w][13] = wcb;
         }
         // the lane holding the wave's last table hit per family hands over its payload
         if (v[11] && lm4 == v[11])
@@ -1221,10 +1223,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             for (int j = 3; j < kPayWords; ++j) s_pay[w][j] = s_lpay[tid][j];
     }
     STAMP(9);
-    // A bare barrier: LDS drained (lgkmcnt), global stores left in flight.  Nothing after this
-    // point reads the frames or verdicts this workgroup wrote, except the last workgroup's
-    // repair pass, and waves holding such packets drained and flagged their stores in the loop;
-    // __syncthreads() would make every wave wait for its write acknowledgements.
+    // A bare barrier: LDS drained (lgkmcnt), global stores left in flight (nothing in this launch
+    // reads what this workgroup wrote; __syncthreads() would make every wave wait for its write
+    // acknowledgements).
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     STAMP(10);
 
@@ -1238,53 +1239,36 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (v) atomicAdd(&rep[k], (unsigned long long)v);
         }
     }
-    if (wave == 0) {
+    if (wave != 0) return;
     // ---- wave 0: flush the workgroup into the replicated accumulators ----
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
     // so every accumulator kind goes out as ONE instruction, lane k carrying field k.  Nothing
-    // waits for them: the next launch reads them (kernel boundary), the host reads them after a
+    // waits for them: the next launch reads them (kernel boundary), the host after a
     // synchronisation.
-    DevState* S = a.st;
     const uint32_t rep = blockIdx.x % kReps;
-    uint32_t cb = 0, x4 = 0, x6 = 0;
+    uint32_t x4 = 0, x6 = 0, f4 = kNone, f6 = kNone, fc = kNone;
     int w4 = 0, w6 = 0;
 #pragma unroll
     for (int v = 0; v < kWaves; ++v) {
-        cb |= s_wv[v][13];
         if (s_wv[v][11] > x4) { x4 = s_wv[v][11]; w4 = v; }
         if (s_wv[v][12] > x6) { x6 = s_wv[v][12]; w6 = v; }
+        f4 = min(f4, s_wv[v][8]);
+        f6 = min(f6, s_wv[v][9]);
+        fc = min(fc, s_wv[v][10]);
     }
-    const bool look = look4 || look6;
-    const bool flag = look && cb;
     if (!(kAblate & 4)) {
-        uint32_t cv = 0, tv = 0;   // lane c < C_N: counter c; lane j < 8: total j
+        uint32_t cv = 0;   // lane c < C_N: counter c of this workgroup
 #pragma unroll
-        for (int v = 0; v < kWaves; ++v) {
-            cv += lane < C_N ? s_wv[v][lane] : 0u;
-            tv += lane >= 1 && lane < 8 ? s_wv[v][lane - 1] : 0u;
-        }
+        for (int v = 0; v < kWaves; ++v) cv += lane < C_N ? s_wv[v][lane] : 0u;
         if (lane < C_N && cv) atomicAdd(&a.acc_cur->cnt[rep][lane], cv);
-        // cumulative totals in upe_counters_t order: pkts_in (the batch size, by workgroup 0),
-        // then C_PARSED .. C_ARP_REPLY
-        if (lane == 0 && blockIdx.x == 0) tv = a.n;
-        if (lane < 8 && tv) atomicAdd(&S->totals[rep][lane], (unsigned long long)tv);
-        // L1 outcome: first miss-then-hit (min) and last table hit (max) per family
-        uint32_t f4 = kNone, f6 = kNone, fc = kNone;
-#pragma unroll
-        for (int v = 0; v < kWaves; ++v) {
-            f4 = min(f4, s_wv[v][8]);
-            f6 = min(f6, s_wv[v][9]);
-            fc = min(fc, s_wv[v][10]);
-        }
-        uint32_t* r4 = reinterpret_cast<uint32_t*>(&a.acc_cur->l1r[rep]);
-        if ((lane == 0 && f4 != kNone) || (lane == 1 && f6 != kNone))
-            atomicMin(r4 + lane, lane == 0 ? f4 : f6);
-        if ((lane == 2 && x4) || (lane == 3 && x6)) atomicMax(r4 + lane, lane == 2 ? x4 : x6);
-        if (lane == 4 && fc != kNone) atomicMin(&a.acc_cur->ctrl[rep], fc);
+        // the L1 outcome, one atomicMax instruction: minima as kNone - x
+        const uint32_t rv = lane == R_F4 ? kNone - f4 : lane == R_F6 ? kNone - f6
+                          : lane == R_M4 ? x4 : lane == R_M6 ? x6 : kNone - fc;
+        if (lane <= R_CTRL && rv) atomicMax(&a.acc_cur->l1r[rep][lane], rv);
         if (lds_stats && small_stats) {
             for (uint32_t k = lane; k < 2 * a.nrules_pad; k += 64) {
                 const uint32_t v = lds_hist[k];
-                if (v) atomicAdd(&S->acc_stats[rep][k], (unsigned long long)v);
+                if (v) atomicAdd(&a.st->acc_stats[rep][k], (unsigned long long)v);
             }
         }
     }
@@ -1292,48 +1276,37 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // maximum points at)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
         reinterpret_cast<uint32_t*>(&a.pay[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
-    uint32_t last = 0;
-    if (look && !(kAblate & 128)) {
-        // A starting entry disagrees with the table: packets of this batch aimed at it take the
-        // entry's MAC only if no earlier packet missed the entry and hit the table, which the
-        // last workgroup to arrive decides.  Arrival tickets carry whether anyone holds such
-        // packets (bits 16..), so that workgroup repairs only when there is something to repair.
-        if (flag) {
-            // publish this workgroup's verdicts and records / frames (release: write back this
-            // XCD's L2)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        }
-        STAMP(5);
-        // every atomic of this workgroup is performed before its arrival ticket
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(6);
-        if (lane == 0) {
-            const uint32_t nb = gridDim.x;
-            const uint32_t sh = blockIdx.x % kShards;
-            const uint32_t nsh = nb < (uint32_t)kShards ? nb : (uint32_t)kShards;
-            const uint32_t per = nb / kShards + (sh < nb % kShards ? 1u : 0u);
-            const uint32_t mine = 1u | (flag ? 0x10000u : 0u);
-            const uint32_t os = __hip_atomic_fetch_add(&S->tickets.shard[sh][0], mine,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((os & 0xFFFFu) == per - 1) {
-                const uint32_t sc = (os >> 16) + (mine >> 16);
-                const uint32_t up = 1u | (sc ? 0x10000u : 0u);
-                const uint32_t ot = __hip_atomic_fetch_add(&S->tickets.top[0], up,
-                                                           __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                if ((ot & 0xFFFFu) == nsh - 1) last = 1u | ((((ot >> 16) + (up >> 16)) ? 1u : 0u) << 1);
-            }
+    STAMP(5);
+    // Batch k - 1's counters into the cumulative totals (upe_counters_t order): total j by
+    // workgroup j % grid (j = 0 the batch size, pkts_in; j >= 1 counter j - 1); one writer per
+    // word, nobody else reads them in this launch.
+    if (blockIdx.x < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((uint32_t)j % gridDim.x != blockIdx.x) continue;
+            const uint32_t v = j == 0 ? *as_const<uint32_t>(&a.acc_prev->n)
+                                      : wave_reduce<0>(lane < kReps ? a.acc_prev->cnt[lane][j - 1]
+                                                                    : 0u);
+            if (lane == 0 && v) a.st->totals[j] += v;
         }
     }
-    if (lane == 0) s_last = last;
-    STAMP(7);
-    }   // wave 0
-    if (!(look4 || look6)) return;
-    // the other waves wait here, so the last workgroup repairs with all its threads
-    __syncthreads();
-    if (!s_last) return;
-    batch_tail<kEmit>(a, tid, look4, look6, (s_last & 2u) != 0, L1);
-    STAMP(8);
+    if (blockIdx.x == 0) {
+        // workgroup 0: the folded starting state for batch k + 1, this batch's grid and size,
+        // batch k + 1's accumulators re-armed
+        if (lane == 0) {
+            uint4* o = reinterpret_cast<uint4*>(a.l1_out);
+            o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
+            o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
+            o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
+            o[3] = make_uint4(0u, 0u, 0u, 0u);
+            a.acc_cur->grid = gridDim.x;
+            a.acc_cur->n = a.n;
+        }
+        uint32_t* nc = &a.acc_next->cnt[0][0];
+        uint32_t* nr = &a.acc_next->l1r[0][0];
+        for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
+        for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0u;
+    }
 }
 
 
@@ -1605,7 +1578,7 @@ struct upe_gpu_ctx {
     TilePay* pay = nullptr;        // [2][paycap] per-workgroup last-hit payloads, by batch parity
     uint32_t paycap = 0;           // largest grid
     // per-batch scratch
-    uint32_t* cand_tile = nullptr; // [ntiles], zero between batches
+    uint32_t* lb = nullptr;        // [tiles_alloc * kWaves] look-back flags (zeroed at allocation)
     size_t tiles_alloc = 0;
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
@@ -1701,10 +1674,10 @@ int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector
 int publish(upe_gpu_ctx* c) {
     struct {
         TilePay* pay;
-        uint32_t* cand_tile;
+        uint32_t* lb;
         unsigned long long* stats;
         unsigned long long* stats_idx;
-    } p = {c->pay, c->cand_tile, c->stats, c->stats_idx};
+    } p = {c->pay, c->lb, c->stats, c->stats_idx};
     static_assert(offsetof(DevState, stats_idx) - offsetof(DevState, pay) == 3 * sizeof(void*),
                   "DevState pointer block");
     HIP_TRY(hipMemcpy(reinterpret_cast<char*>(c->st) + offsetof(DevState, pay), &p, sizeof p,
@@ -1714,12 +1687,12 @@ int publish(upe_gpu_ctx* c) {
 
 int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
     if (ntiles > c->tiles_alloc) {
-        if (c->cand_tile) (void)hipFree(c->cand_tile);
-        c->cand_tile = nullptr;
+        if (c->lb) (void)hipFree(c->lb);
+        c->lb = nullptr;
         c->tiles_alloc = 0;
         size_t want = ntiles + ntiles / 4 + 16;
-        HIP_TRY(hipMalloc(&c->cand_tile, want * sizeof(uint32_t)));
-        HIP_TRY(hipMemset(c->cand_tile, 0, want * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&c->lb, want * kWaves * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(c->lb, 0, want * kWaves * sizeof(uint32_t)));
         c->tiles_alloc = want;
         if (publish(c) != 0) return -1;
     }
@@ -1763,17 +1736,11 @@ int l1_sync(upe_gpu_ctx* c) {
 }
 
 // The between-batch state of a fresh context (a calloc'd worker_t): L1 all zero, accumulators
-// armed (nothing happened), tickets and totals zero.
+// armed (nothing happened), totals zero.
 int arm_state(upe_gpu_ctx* c) {
     if (order_on(c, c->stream) != 0) return -1;
     static DevState init;   // zero, then the armed accumulator fields
-    for (auto& acc : init.acc) {
-        for (int r = 0; r < kReps; ++r) {
-            acc.l1r[r] = make_uint4(kNone, kNone, 0u, 0u);
-            acc.ctrl[r] = kNone;
-        }
-        acc.grid = 1;
-    }
+    for (auto& acc : init.acc) acc.grid = 1;   // every other word zero: nothing happened
     HIP_TRY(hipMemcpyAsync(c->st, &init, offsetof(DevState, pay), hipMemcpyHostToDevice,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1784,6 +1751,18 @@ int arm_state(upe_gpu_ctx* c) {
 
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// A look-back that gave up means the persistent grid was not resident: report it once.
+int check_lookback(upe_gpu_ctx* c) {
+    uint32_t t = 0;
+    HIP_TRY(hipMemcpy(&t, &c->st->lb_timeout, sizeof t, hipMemcpyDeviceToHost));
+    if (t) {
+        HIP_TRY(hipMemset(&c->st->lb_timeout, 0, sizeof t));
+        return fail("a look-back wait gave up: the persistent grid was not resident "
+                    "(results of that batch are not exact)");
+    }
+    return 0;
+}
 
 void launch_classify(bool tss, bool emit, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
     if (tss && emit)
@@ -1846,6 +1825,9 @@ uint32_t resident_grid(upe_gpu_ctx* c, bool tss, bool emit, size_t lds, hipStrea
     }
     if (grid > c->paycap) grid = c->paycap;
     c->resident[key] = grid;
+    if (getenv("UPE_GPU_VERBOSE"))
+        fprintf(stderr, "upe_gpu: persistent grid %u (occupancy API %d per CU, lds %zu, tss %d, "
+                "emit %d)\n", grid, per_cu, lds, (int)tss, (int)emit);
     return grid;
 }
 
@@ -1932,7 +1914,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->stats_pk, c->lens16, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->cand_tile, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
+                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2424,7 +2406,10 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.acc_cur = acc_slot(c, c->k);
     a.acc_prev = acc_slot(c, c->k + 2);
     a.acc_next = acc_slot(c, c->k + 1);
-    a.cand_tile = c->cand_tile;
+    a.lb = c->lb;
+    a.lb_tag = (uint32_t)(c->k % kLbTagMod) + 1u;
+    if (c->k > 0 && c->k % kLbTagMod == 0)   // tags wrap: no flag may carry this launch's tag
+        HIP_TRY(hipMemsetAsync(c->lb, 0, c->tiles_alloc * kWaves * sizeof(uint32_t), s));
     a.stats = c->stats;
     a.stats_idx = c->stats_idx;
     a.flow_hash = d_flow_hash;
@@ -2836,7 +2821,7 @@ int upe_gpu_sync(upe_gpu_ctx_t* c, void* stream) {
     if (!c) return fail("null context");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(pick(c, stream)));
-    return 0;
+    return check_lookback(c);
 }
 
 int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
@@ -2849,14 +2834,14 @@ int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
     BatchAcc b;   // the last batch's accumulators
     HIP_TRY(hipMemcpy(&b, acc_slot(c, c->k + 2), sizeof b, hipMemcpyDeviceToHost));
     uint64_t* dst = &info->counters.pkts_in;
-    dst[0] = c->last_n;
-    uint32_t first = kNone;
+    dst[0] = b.n;
+    uint32_t cm = 0;
     for (int r = 0; r < kReps; ++r) {
         for (int j = 0; j < 7; ++j) dst[1 + j] += b.cnt[r][j];
         info->n_ctrl += b.cnt[r][C_CTRL];
-        first = std::min(first, b.ctrl[r]);
+        cm = std::max(cm, b.l1r[r][R_CTRL]);
     }
-    if (first != kNone) info->first_ctrl = first;
+    if (cm) info->first_ctrl = kNone - cm;
     return 0;
 }
 
@@ -2865,13 +2850,19 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
     if (!c) return fail("null context");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
+    if (check_lookback(c) != 0) return -1;
     if (counters) {
-        unsigned long long t[kReps][8];
-        HIP_TRY(hipMemcpy(t, &c->st->totals[0][0], sizeof t, hipMemcpyDeviceToHost));
+        // the totals up to batch k - 2, plus batch k - 1 (folded in by the next launch)
+        unsigned long long t[8];
+        HIP_TRY(hipMemcpy(t, &c->st->totals[0], sizeof t, hipMemcpyDeviceToHost));
         uint64_t* dst = &counters->pkts_in;
-        for (int j = 0; j < 8; ++j) {
-            dst[j] = 0;
-            for (int r = 0; r < kReps; ++r) dst[j] += t[r][j];
+        for (int j = 0; j < 8; ++j) dst[j] = t[j];
+        if (c->k > 0) {
+            BatchAcc b;
+            HIP_TRY(hipMemcpy(&b, acc_slot(c, c->k + 2), sizeof b, hipMemcpyDeviceToHost));
+            dst[0] += b.n;
+            for (int r = 0; r < kReps; ++r)
+                for (int j = 0; j < 7; ++j) dst[1 + j] += b.cnt[r][j];
         }
     }
     if (rule_stats) {
@@ -2897,7 +2888,12 @@ int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
     if (!c) return fail("null context");
     HIP_TRY(hipSetDevice(c->device));
     if (order_on(c, c->stream) != 0) return -1;
-    HIP_TRY(hipMemsetAsync(&c->st->totals[0][0], 0, sizeof(c->st->totals), c->stream));
+    HIP_TRY(hipMemsetAsync(&c->st->totals[0], 0, sizeof(c->st->totals), c->stream));
+    if (c->k > 0) {   // the last batch's counters, not yet folded into the totals
+        BatchAcc* b = acc_slot(c, c->k + 2);
+        HIP_TRY(hipMemsetAsync(&b->cnt[0][0], 0, sizeof(b->cnt), c->stream));
+        HIP_TRY(hipMemsetAsync(&b->n, 0, sizeof(b->n), c->stream));
+    }
     HIP_TRY(hipMemsetAsync(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats), c->stream));
     HIP_TRY(hipMemsetAsync(c->stats, 0, c->cap * 2 * sizeof(unsigned long long), c->stream));
     if (c->stats_idx)
