@@ -308,7 +308,10 @@ int upe_gpu_compact(upe_gpu_ctx_t *ctx, const uint32_t *d_verdict, size_t n, uin
  * tables are), the new snapshot is uploaded, and the next segment runs.  Control packets are
  * found on the device (one marking pass plus an ordered compaction), so a batch without them
  * costs one extra pass.  Synchronous; *n_writes (optional) = table writes applied.  Capacities
- * are powers of two, as arp_table_init / ndp_table_init require. */
+ * are powers of two, as arp_table_init / ndp_table_init require.  The NS/NA option walk reads
+ * the whole frame (len bytes), so this call needs FULL frames: a batch of UPE_FRAME_TAIL-byte
+ * header windows (upe_gpu_process_host's window form) is not valid here — an NS/NA longer than
+ * its window would have its options read from the bytes that follow the window. */
 int upe_gpu_process_segmented(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                               uint32_t *d_verdict, size_t n, upe_arp_entry_t *arp,
                               size_t arp_capacity, upe_ndp_entry_t *ndp, size_t ndp_capacity,

@@ -8,13 +8,17 @@
  * What it shows: a reference worker_t, fed through the reference SPSC ring by an RX-like
  * producer thread exactly as src/rx_pcap.c feeds it (pktbuf_alloc, memcpy, ring_push_burst),
  * runs a GPU-backed worker loop instead of src/worker.c:255-307 — ring_pop_burst bursts
- * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch, then
- * the reference's TX accounting (tx_send_batch, pkts_forwarded / pkts_dropped, pktbuf_free) —
- * and ends with the same counters and rule_stats in the same worker_t fields the reference's
- * stats thread reads (src/main.c:293-315).  tests/test_gpu_dropin.py compares them with the
- * reference worker itself (oracle/_ref/libupe_ref.so) on the same packets.
+ * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch (cut
+ * after every packet that writes a neighbour table, whose write is then applied with the
+ * reference's own arp_update / ndp_update and the snapshot re-uploaded), then the reference's TX
+ * accounting (tx_send_batch, pkts_forwarded / pkts_dropped, pktbuf_free, tx_send of ARP
+ * replies) — and ends with the same counters and rule_stats in the same worker_t fields the
+ * reference's stats thread reads (src/main.c:293-315).  tests/test_gpu_dropin.py compares
+ * them, every packet's bytes and the final neighbour tables with the reference worker itself
+ * (oracle/_ref/libupe_ref.so) on the same packets, control packets included.
  */
 #define _GNU_SOURCE
+#include <arpa/inet.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdlib.h>
@@ -63,23 +67,112 @@ static void flush_tx(worker_t *w) {
     }
 }
 
+/* Byte k of a frame as a zero-filled pktbuf holds it (the reference reads the ethertype and the
+ * ARP header without a length check, src/worker.c:24-35). */
+static uint8_t at(const pktbuf_t *b, size_t k) { return k < b->len ? b->data[k] : 0; }
+
+/* A packet handle_control_packet may write a neighbour table for (src/worker.c:28-39, 57-100):
+ * ARP with the Ethernet/IPv4 header shape, or an IPv6 NS/NA of at least 78 bytes.  The batch is
+ * cut after it, so every later packet sees the table write, as in the reference's burst loop. */
+static int is_table_write(const pktbuf_t *b) {
+    const unsigned et = (unsigned)at(b, 12) << 8 | at(b, 13);
+    if (et == 0x0806)
+        return at(b, 14) == 0 && at(b, 15) == 1 && at(b, 16) == 8 && at(b, 17) == 0 &&
+               at(b, 18) == 6 && at(b, 19) == 4;
+    return et == 0x86DD && b->len >= 78 && at(b, 20) == 58 && (at(b, 54) == 135 || at(b, 54) == 136);
+}
+
+/* handle_control_packet's table writes and ARP reply (src/worker.c:30-52, 64-95) for a packet the
+ * GPU classified: v is its verdict, b->data the frame as the GPU left it (an answered ARP request
+ * already rewritten into the reply, whose tha / tpa now hold the request's sha / spa). */
+static void control_writes(worker_t *w, pktbuf_t *b, uint32_t v) {
+    const uint8_t *d = b->data;
+    if (v & UPE_VF_ARP_LEARN) {
+        const int replied = (v & UPE_VF_ARP_REPLY) != 0;
+        uint32_t spa_be;
+        memcpy(&spa_be, d + (replied ? 38 : 28), 4);
+        arp_update(w->arpt, ntohl(spa_be), d + (replied ? 32 : 22));
+        if (replied) tx_send(w->tx, b->data, b->len);
+    } else if (UPE_VERDICT_CODE(v) == UPE_V_CONSUMED) {
+        const int ns = d[54] == 135;
+        for (size_t off = 78; off + 2 <= b->len;) {
+            const uint8_t type = d[off];
+            const size_t olen = (size_t)d[off + 1] * 8;
+            if (olen == 0 || off + olen > b->len) break;
+            if (olen >= 8 && ((ns && type == 1) || (!ns && type == 2))) {
+                ndp_update(w->ndpt, ns ? d + 22 : d + 62, d + off + 2);
+                break;
+            }
+            off += olen;
+        }
+    }
+}
+
+static int load_tables(upe_gpu_ctx_t *ctx, worker_t *w) {
+    pthread_rwlock_rdlock(&w->arpt->lock);
+    pthread_rwlock_rdlock(&w->ndpt->lock);
+    int rc = upe_gpu_load_neigh(ctx, (const upe_arp_entry_t *)w->arpt->entries, w->arpt->capacity,
+                                (const upe_ndp_entry_t *)w->ndpt->entries, w->ndpt->capacity);
+    pthread_rwlock_unlock(&w->ndpt->lock);
+    pthread_rwlock_unlock(&w->arpt->lock);
+    return rc;
+}
+
+typedef struct {
+    upe_gpu_ctx_t *ctx;
+    uint8_t *win;
+    uint64_t *desc;
+    uint32_t *verdict;
+    pktbuf_t **bufs;
+    size_t n;
+} gpu_batch_t;
+
+/* One GPU batch through the host round trip, then the reference's per-verdict handling
+ * (src/worker.c:146-153 drops, :240-243 TX queue, :96-98 consumed) and, when the batch ends with
+ * a table-writing control packet, that packet's writes and the new table snapshot. */
+static int run_batch(worker_t *w, gpu_batch_t *g, int cut) {
+    if (g->n == 0) return 0;
+    if (upe_gpu_process_host(g->ctx, g->win, g->n * WIN + UPE_FRAME_TAIL, g->desc, g->verdict,
+                             g->n, 0) != 0)
+        return -1;
+    for (size_t i = 0; i < g->n; i++) {
+        pktbuf_t *b = g->bufs[i];
+        const uint32_t v = g->verdict[i];
+        memcpy(b->data, g->win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
+        if (cut && i + 1 == g->n) control_writes(w, b, v);
+        if (UPE_VERDICT_CODE(v) == UPE_V_FWD) {
+            w->tx_frames[w->tx_count] = b->data; /* worker.c:240-243 */
+            w->tx_lens[w->tx_count] = b->len;
+            w->tx_bufs[w->tx_count++] = b;
+            if (w->tx_count == WORKER_BURST_SIZE) flush_tx(w);
+        } else if (UPE_VERDICT_CODE(v) == UPE_V_CONSUMED) {
+            pktbuf_free(w->pool, b); /* consumed control packet: no counter */
+        } else {
+            w->pkts_dropped++; /* every drop path of process_packet counts one */
+            pktbuf_free(w->pool, b);
+        }
+    }
+    flush_tx(w);
+    g->n = 0;
+    return cut ? load_tables(g->ctx, w) : 0;
+}
+
 /* GPU-backed replacement of worker_main (reference src/worker.c:255-307). */
 static void *gpu_worker_main(void *arg) {
     gpu_arg_t *ga = arg;
     worker_t *w = ga->w;
     ga->rc = -1;
-    upe_gpu_ctx_t *ctx = upe_gpu_open(ga->device, w->rt->capacity);
-    uint8_t *win = upe_gpu_host_alloc((size_t)GPU_BATCH * WIN + UPE_FRAME_TAIL);
-    uint64_t *desc = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint64_t));
-    uint32_t *verdict = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint32_t));
-    pktbuf_t **bufs = malloc(GPU_BATCH * sizeof(*bufs));
-    if (!ctx || !win || !desc || !verdict || !bufs) return NULL;
-    if (upe_gpu_load_rules(ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
-        upe_gpu_load_neigh(ctx, (const upe_arp_entry_t *)w->arpt->entries, w->arpt->capacity,
-                           (const upe_ndp_entry_t *)w->ndpt->entries, w->ndpt->capacity) != 0 ||
-        upe_gpu_set_port(ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0)
+    gpu_batch_t g;
+    memset(&g, 0, sizeof g);
+    g.ctx = upe_gpu_open(ga->device, w->rt->capacity);
+    g.win = upe_gpu_host_alloc((size_t)GPU_BATCH * WIN + UPE_FRAME_TAIL);
+    g.desc = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint64_t));
+    g.verdict = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint32_t));
+    g.bufs = malloc(GPU_BATCH * sizeof(*g.bufs));
+    if (!g.ctx || !g.win || !g.desc || !g.verdict || !g.bufs) return NULL;
+    if (upe_gpu_load_rules(g.ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
+        load_tables(g.ctx, w) != 0 || upe_gpu_set_port(g.ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0)
         return NULL;
-    size_t n = 0;
     void *burst[WORKER_BURST_SIZE];
     for (;;) {
         unsigned k = ring_pop_burst(w->rx_ring, burst, WORKER_BURST_SIZE); /* worker.c:268 */
@@ -87,47 +180,28 @@ static void *gpu_worker_main(void *arg) {
         for (unsigned j = 0; j < k; j++) {
             pktbuf_t *b = burst[j];
             size_t c = b->len < WIN ? b->len : WIN;
-            memcpy(win + n * WIN, b->data, c);
-            memset(win + n * WIN + c, 0, WIN - c);
-            desc[n] = UPE_DESC((uint64_t)n * WIN, b->len);
-            bufs[n++] = b;
+            memcpy(g.win + g.n * WIN, b->data, c);
+            memset(g.win + g.n * WIN + c, 0, WIN - c);
+            g.desc[g.n] = UPE_DESC((uint64_t)g.n * WIN, b->len);
+            g.bufs[g.n++] = b;
+            const int cut = is_table_write(b);
+            if ((cut || g.n == GPU_BATCH) && run_batch(w, &g, cut) != 0) return NULL;
         }
         const int stop = k == 0 && g_stop;
-        if (n == GPU_BATCH || (k == 0 && n > 0)) {
-            if (upe_gpu_process_host(ctx, win, (size_t)n * WIN + UPE_FRAME_TAIL, desc, verdict,
-                                     n, 0) != 0)
-                return NULL;
-            for (size_t i = 0; i < n; i++) {
-                pktbuf_t *b = bufs[i];
-                memcpy(b->data, win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
-                if (UPE_VERDICT_CODE(verdict[i]) == UPE_V_FWD) {
-                    w->tx_frames[w->tx_count] = b->data; /* worker.c:240-243 */
-                    w->tx_lens[w->tx_count] = b->len;
-                    w->tx_bufs[w->tx_count++] = b;
-                    if (w->tx_count == WORKER_BURST_SIZE) flush_tx(w);
-                } else if (UPE_VERDICT_CODE(verdict[i]) == UPE_V_CONSUMED) {
-                    pktbuf_free(w->pool, b); /* consumed control packet: no counter */
-                } else {
-                    w->pkts_dropped++; /* every drop path of process_packet counts one */
-                    pktbuf_free(w->pool, b);
-                }
-            }
-            flush_tx(w);
-            n = 0;
-        }
+        if (k == 0 && g.n > 0 && run_batch(w, &g, 0) != 0) return NULL;
         if (stop) break;
     }
     /* the counters the GPU keeps, into the reference's own worker_t fields */
     upe_counters_t c;
-    if (upe_gpu_get_stats(ctx, &c, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity) != 0)
+    if (upe_gpu_get_stats(g.ctx, &c, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity) != 0)
         return NULL;
     w->pkts_parsed = c.pkts_parsed;
     w->pkts_matched = c.pkts_matched;
-    upe_gpu_host_free(win);
-    upe_gpu_host_free(desc);
-    upe_gpu_host_free(verdict);
-    free(bufs);
-    upe_gpu_close(ctx);
+    upe_gpu_host_free(g.win);
+    upe_gpu_host_free(g.desc);
+    upe_gpu_host_free(g.verdict);
+    free(g.bufs);
+    upe_gpu_close(g.ctx);
     ga->rc = 0;
     return NULL;
 }
@@ -136,13 +210,16 @@ static void *gpu_worker_main(void *arg) {
  * Run `n` packets (batch layout of include/upe_gpu.h) through: an RX-like producer thread ->
  * reference SPSC ring -> reference worker_t driven by gpu_worker_main.  rules in insertion order
  * (rule_table_add), neighbour slot arrays copied into reference tables.  Outputs the worker's
- * counters (pkts_in, parsed, matched, forwarded, dropped) and rule_stats[capacity].
+ * counters (pkts_in, parsed, matched, forwarded, dropped), rule_stats[capacity], each packet's
+ * bytes as the worker left them in its pktbuf (out_frames, the input's layout) and the final
+ * neighbour slot arrays (out_arp / out_ndp, the input capacities).
  */
 int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
                    const upe_arp_entry_t *arp, size_t arp_cap, const upe_ndp_entry_t *ndp,
                    size_t ndp_cap, const uint8_t eth_addr[6], uint32_t ip4_addr,
                    const uint8_t *frames, const uint64_t *in_desc, size_t n, int device,
-                   uint64_t counters[5], upe_rule_stat_t *rule_stats) {
+                   uint64_t counters[5], upe_rule_stat_t *rule_stats, uint8_t *out_frames,
+                   upe_arp_entry_t *out_arp, upe_ndp_entry_t *out_ndp) {
     rule_table_t rt;
     if (rule_table_init(&rt, capacity) != 0) return -1;
     for (size_t i = 0; i < nrules; i++)
@@ -202,6 +279,11 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     counters[3] = w->pkts_forwarded;
     counters[4] = w->pkts_dropped;
     if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
+    if (out_frames)
+        for (size_t i = 0; i < n; i++)
+            memcpy(out_frames + (size_t)(in_desc[i] >> 16), all[i]->data, (size_t)(in_desc[i] & 0xFFFF));
+    if (out_arp && arp_cap) memcpy(out_arp, arpt.entries, arp_cap * sizeof(arp_entry_t));
+    if (out_ndp && ndp_cap) memcpy(out_ndp, ndpt.entries, ndp_cap * sizeof(ndp_entry_t));
     worker_destroy(w);
     free(w);
     free(all);

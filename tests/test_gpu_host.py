@@ -103,3 +103,28 @@ def test_host_roundtrip_rejects_short_buffer(gpu_worker_factory):
             w.process_host(wl.frames[: int(desc_offsets(wl.desc)[-1]) + 8].copy(), wl.desc, verdict)
     finally:
         w.close()
+
+
+@pytest.mark.parametrize("chunk", [257, 4096])
+def test_host_roundtrip_permuted_descriptors(gpu_worker_factory, chunk):
+    """Descriptors in pool order, not address order (include/upe_gpu.h allows any order): every
+    chunk's byte span interleaves with its neighbours', so a chunk's copy-back also rewrites
+    frames of the chunks before and after it.  The round trip must wait for those and end with
+    exactly the oracle's bytes for every frame."""
+    import dataclasses
+
+    base = synth.config_c(n=60_000, seed=71)
+    perm = np.random.default_rng(71).permutation(base.n)
+    wl = dataclasses.replace(base, desc=np.ascontiguousarray(base.desc[perm]))
+    r = oracle.run_restated(wl)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        frames = wl.frames.copy()
+        verdict = np.zeros(wl.n, np.uint32)
+        w.process_host(frames, wl.desc, verdict, chunk)
+        _check(w, wl, frames, verdict, {"verdict": r.verdict, "frames": r.frames,
+                                        "counters": r.counters, "rule_stats": r.rule_stats,
+                                        "l1": r.l1}, f"permuted chunk={chunk}")
+    finally:
+        w.close()

@@ -41,6 +41,23 @@ for rep in range(6):
     rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
     print(f"rep {rep}: grid {st.shape[0]} WGs; end of kernel ~{rel[:, 7].max():.2f} us; tail end "
           f"{rel[:, 8].max():.2f} us")
+    if rep == 5:
+        # where the loop-end spread comes from: by blockIdx % 8 (the XCD group) and by start time
+        loop = rel[:, 4]
+        ent = rel[:, 0]
+        b = np.nonzero(valid)[0]
+        for g in range(8):
+            sel = (b % 8) == g
+            print(f"   xcd-group {g}: loop end med {np.median(loop[sel]):6.2f} max {loop[sel].max():6.2f}"
+                  f"  entry med {np.median(ent[sel]):5.2f}")
+        order = np.argsort(ent)
+        q = np.array_split(order, 4)
+        for k, idx in enumerate(q):
+            print(f"   entry quartile {k}: entry {np.median(ent[idx]):5.2f} loop end med "
+                  f"{np.median(loop[idx]):6.2f} max {loop[idx].max():6.2f}")
+        print("   corr(entry, loop end) =", round(float(np.corrcoef(ent, loop)[0, 1]), 3))
+        last = np.argsort(loop)[-10:]
+        print("   10 latest loop ends: blocks", b[last].tolist(), "entry", np.round(ent[last], 2).tolist())
     for j, nm in enumerate(names):
         col = rel[:, j]
         col = col[col >= 0]

@@ -141,14 +141,15 @@ struct DevL1 {
 // totals, which the host sums when it reads them.  No workgroup ever waits for another.
 enum { C_PARSED, C_MATCHED, C_FWD, C_DROPPED, C_CONSUMED, C_ARP_LEARN, C_ARP_REPLY, C_CTRL, C_N };
 // l1r words, all combined with atomicMax (minima stored as kNone - x, so "none" is 0)
-enum { R_F4, R_F6, R_M4, R_M6, R_CTRL, R_N = 8 };
+enum { R_F4, R_F6, R_M4, R_M6, R_N };
 struct __attribute__((aligned(128))) BatchAcc {
-    uint32_t cnt[kReps][C_N];   // this batch's counters
-    uint32_t l1r[kReps][R_N];   // R_F4 / R_F6: kNone - first miss-then-hit index v4 / v6;
-                                // R_M4 / R_M6: last table hit v4 / v6 (index + 1, 0 = none);
-                                // R_CTRL: kNone - first control packet
-    uint32_t grid;              // the batch's grid (which workgroup holds a payload)
-    uint32_t n;                 // the batch's size
+    uint32_t cnt[kReps][C_N];              // this batch's counters
+    unsigned long long l1r[kReps][R_N];    // R_F4 / R_F6: kNone - first miss-then-hit index
+                                           // v4 / v6; R_M4 / R_M6: last table hit v4 / v6 as
+                                           // (index + 1) << 32 | the workgroup holding its payload
+    uint32_t ctrl[kReps];                  // kNone - first control packet (max)
+    uint32_t grid;                         // the batch's grid
+    uint32_t n;                            // the batch's size
     uint32_t pad[30];
 };
 // Payload of a workgroup's last table hit per family; the next batch reads the one the batch
@@ -234,17 +235,26 @@ struct Args {
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
     uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
-    // this batch's slots of the between-batch state (DevState comment)
-    const DevL1* l1_in;
-    DevL1* l1_out;
-    BatchAcc* acc_cur;
-    const BatchAcc* acc_prev;
-    BatchAcc* acc_next;
-    const TilePay* pay_prev;
-    uint32_t* census;                // non-null: a residency census launch (census_probe) only
+    // this batch's slots of the between-batch state (DevState comment) follow from k6 = k % 6
+    // (pointers computed where they are used: the kernel's scalar registers are scarce)
+    uint32_t k6;
+    uint32_t paycap;                 // a.pay[(k % 2) * paycap + workgroup]
+    uint32_t census;                 // non-zero: a residency census launch (census_probe) only
     uint32_t* lb;                    // look-back flags [ntiles * kWaves]
     uint32_t lb_tag;                 // this launch's flag tag
 };
+// Batch k's state slots, from Args (DevState comment).
+__device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
+__device__ __forceinline__ DevL1* l1_out(const Args& a) { return &a.st->l1[(a.k6 + 1) % 2]; }
+__device__ __forceinline__ BatchAcc* acc_cur(const Args& a) { return &a.st->acc[a.k6 % 3]; }
+__device__ __forceinline__ const BatchAcc* acc_prev(const Args& a) { return &a.st->acc[(a.k6 + 2) % 3]; }
+__device__ __forceinline__ BatchAcc* acc_next(const Args& a) { return &a.st->acc[(a.k6 + 1) % 3]; }
+__device__ __forceinline__ TilePay* pay_cur(const Args& a) {
+    return a.pay + (size_t)(a.k6 % 2) * a.paycap;
+}
+__device__ __forceinline__ const TilePay* pay_prev(const Args& a) {
+    return a.pay + (size_t)((a.k6 + 1) % 2) * a.paycap;
+}
 
 // ---- diagnostic timestamps (UPE_STAMPS builds only; never in the product build) ------------
 #ifndef UPE_STAMPS
@@ -424,23 +434,41 @@ __device__ __forceinline__ const __attribute__((address_space(4))) V* as_const(c
 // before it, unless some forwarded packet missed the starting entry and hit the table — then
 // the batch's last table hit, whose MAC is the table's (so the entry agrees with the table).
 // in: DevL1 words before the batch; f4 / f6: first miss-then-hit (kNone = none); m4 / m6: last
-// table hit + 1 (0 = none); grid / pay: the batch's grid and per-workgroup last-hit payloads.
+// table hit + 1 (0 = none); wg4 / wg6: the workgroups holding those hits' payloads in pay.
 // All arguments wave-uniform.  L: DevL1 words 0..10 after the batch.
 __device__ __forceinline__ void fold_l1(const u32x16& in, uint32_t f4, uint32_t f6, uint32_t m4,
-                                        uint32_t m6, uint32_t grid, const TilePay* pay,
-                                        uint32_t (&L)[11]) {
+                                        uint32_t m6, uint32_t wg4, uint32_t wg6,
+                                        const TilePay* pay, uint32_t (&L)[11]) {
 #pragma unroll
     for (int j = 0; j < 11; ++j) L[j] = in[j];
     if (f4 != kNone && m4 != 0) {
-        const u32x16 P = *as_const<u32x16>(pay + ((m4 - 1) / kTile) % grid);
+        const u32x16 P = *as_const<u32x16>(pay + wg4);
         L[0] = P[0]; L[1] = P[1]; L[2] = P[2];
         L[9] = 1;
     }
     if (f6 != kNone && m6 != 0) {
-        const u32x16 P = *as_const<u32x16>(pay + ((m6 - 1) / kTile) % grid);
+        const u32x16 P = *as_const<u32x16>(pay + wg6);
         L[3] = P[3]; L[4] = P[4]; L[5] = P[5]; L[6] = P[6]; L[7] = P[7]; L[8] = P[8];
         L[10] = 1;
     }
+}
+
+// The batch's L1 outcome from its replicated l1r words: lane r < kReps holds replica r (lo/hi
+// 32-bit halves of the 64-bit words), the rest zero.  Results wave-uniform.
+struct L1Out {
+    uint32_t f4, f6, m4, m6, wg4, wg6;
+};
+__device__ __forceinline__ L1Out reduce_l1r(const unsigned long long (&w)[R_N]) {
+    L1Out o;
+    o.f4 = kNone - wave_reduce<2>((uint32_t)w[R_F4]);
+    o.f6 = kNone - wave_reduce<2>((uint32_t)w[R_F6]);
+    const uint32_t h4 = (uint32_t)(w[R_M4] >> 32), h6 = (uint32_t)(w[R_M6] >> 32);
+    o.m4 = wave_reduce<2>(h4);
+    o.m6 = wave_reduce<2>(h6);
+    // one packet index, one workgroup: the lanes holding the maximum agree on it
+    o.wg4 = wave_reduce<2>(h4 == o.m4 && o.m4 ? (uint32_t)w[R_M4] : 0u);
+    o.wg6 = wave_reduce<2>(h6 == o.m6 && o.m6 ? (uint32_t)w[R_M6] : 0u);
+    return o;
 }
 
 // Fold a finished batch into the state the next one starts from, on the host's request (before
@@ -448,15 +476,16 @@ __device__ __forceinline__ void fold_l1(const u32x16& in, uint32_t f4, uint32_t 
 // acc's L1 fields back to "nothing happened", so the next launch's own fold is the identity.
 __global__ void upe_l1_sync(DevL1* l1, BatchAcc* acc, const TilePay* pay) {
     const int lane = threadIdx.x;
-    uint4 pr = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < kReps) pr = *reinterpret_cast<const uint4*>(&acc->l1r[lane][0]);
-    const uint32_t f4 = kNone - wave_reduce<2>(pr.x), f6 = kNone - wave_reduce<2>(pr.y);
-    const uint32_t m4 = wave_reduce<2>(pr.z), m6 = wave_reduce<2>(pr.w);
+    unsigned long long w[R_N] = {0, 0, 0, 0};
+    if (lane < kReps)
+        for (int j = 0; j < R_N; ++j) w[j] = acc->l1r[lane][j];
+    const L1Out o = reduce_l1r(w);
     const u32x16 in = *as_const<u32x16>(l1);
     uint32_t L[11];
-    fold_l1(in, f4, f6, m4, m6, acc->grid ? acc->grid : 1u, pay, L);
+    fold_l1(in, o.f4, o.f6, o.m4, o.m6, o.wg4, o.wg6, pay, L);
     __syncthreads();
-    if (lane < kReps) *reinterpret_cast<uint4*>(&acc->l1r[lane][0]) = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < kReps)
+        for (int j = 0; j < R_N; ++j) acc->l1r[lane][j] = 0ull;
     if (lane == 0) {
         uint32_t* w = reinterpret_cast<uint32_t*>(l1);
 #pragma unroll
@@ -613,12 +642,11 @@ struct Parsed {
     uint32_t ttl, c1w1, c1w2;      // TTL / hop, and bytes 20..27 as they are forwarded
 };
 
-// Two forms (only waves holding such a packet run either): inlined, and an out-of-line call.
-// The call saves the caller's live registers to scratch, ~100 bytes of private-memory traffic
-// per slow packet (config D: 1.7 GB written per 16M batch; 2.32 -> 1.82 ms inlined), but keeps
-// the fast path's register allocation lean (config B, which has no slow packets: 34.4 vs
-// 35.1 us inlined).  The tuple-space kernel, used for the large tables of the stress
-// configuration, inlines it; the scan kernel calls it.
+// Inlined (only waves holding such a packet run it).  An out-of-line call (UPE_GP_CALL=1, a
+// diagnostic build) saves the caller's live registers to scratch, ~100 bytes of private-memory
+// traffic per slow packet (config D: 1.7 GB written per 16M batch), and a kernel with a scratch
+// stack depends on the runtime's scratch allocation for its residency; inlined, every classify
+// kernel but one runs without scratch at the 128-VGPR budget.
 struct Port {
     uint32_t mac_lo, mac_hi, ip4;
 };
@@ -753,9 +781,14 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
         }
     }
 }
+#ifndef UPE_GP_CALL
+#define UPE_GP_CALL 0   // 1: the scan kernel calls the general path out of line (scratch stack)
+#endif
+#if UPE_GP_CALL
 __device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len, Parsed& r) {
     general_path(a, p, len, r);
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Decoupled look-back (only while a starting L1 entry disagrees with the table).  A packet whose
@@ -852,7 +885,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
 
     if (a.census) {
-        if (threadIdx.x == 0) census_probe(a.census, gridDim.x);
+        if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
         return;
     }
     if (kAblate & 64) return;
@@ -866,7 +899,27 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
 
-    // the first descriptor, and small rule tables into LDS, before the entry barrier
+    // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past len
+    // are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame costs
+    // four loads, not five.  Frames shorter than 49 bytes never take the fast path.
+    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[20]) {
+#pragma unroll
+        for (int j = 0; j < 20; ++j) w[j] = 0;
+        if (live) {
+            const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
+            const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
+#pragma unroll
+            for (int c = 0; c < 5; ++c) {
+                if (c < 3 || len > 16u * c) {
+                    const uint4 v = q[c];
+                    w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+                }
+            }
+        }
+    };
+    // The first descriptor (its round trip runs under the table staging below), then small
+    // rule tables into LDS, before the entry barrier.  (Issuing the first tile's window loads
+    // here too made the staging wait for them at the barrier: 2.5 us per 1M batch slower.)
     uint64_t dsc_next = 0;
     if (blockIdx.x < a.ntiles && blockIdx.x * kTile + (uint32_t)tid < a.n)
         dsc_next = a.desc[blockIdx.x * kTile + (uint32_t)tid];
@@ -882,10 +935,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // outcome folded in (its replicated minima / maxima, then at most two payload loads).
     // DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4], ndp_mac_lo/hi, arp_ok, ndp_ok.
     static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
-    const u32x16 lin = *as_const<u32x16>(a.l1_in);
-    uint4 pr = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < kReps) pr = *reinterpret_cast<const uint4*>(&a.acc_prev->l1r[lane][0]);
-    const uint32_t pgrid = *as_const<uint32_t>(&a.acc_prev->grid);
+    const u32x16 lin = *as_const<u32x16>(l1_in(a));
+    unsigned long long pr[R_N] = {0, 0, 0, 0};
+    if (lane < kReps)
+        for (int j = 0; j < R_N; ++j) pr[j] = acc_prev(a)->l1r[lane][j];
     // small ARP indexes (<= 16 KB) into LDS after the rule-stats bins: a lookup is then an LDS
     // read, not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
@@ -903,9 +956,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
             for (int j = 0; j < 11; ++j) L1[j] = lin[j];
         } else {
-            fold_l1(lin, kNone - wave_reduce<2>(pr.x), kNone - wave_reduce<2>(pr.y),
-                    wave_reduce<2>(pr.z), wave_reduce<2>(pr.w), pgrid ? pgrid : 1u, a.pay_prev,
-                    L1);
+            const L1Out o = reduce_l1r(pr);
+            fold_l1(lin, o.f4, o.f6, o.m4, o.m6, o.wg4, o.wg6, pay_prev(a), L1);
         }
         look4 = L1[9] == 0u;    // the ARP entry disagrees with the table
         look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
@@ -920,9 +972,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     uint32_t c01 = 0, c23 = 0, c45 = 0, c67 = 0;
     uint32_t lf4 = kNone, lf6 = kNone, lfc = kNone, lm4 = 0, lm6 = 0;
     // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
-    // tiles b, b + grid, ... so the per-workgroup flush and arrival ticket happen once per
-    // workgroup, at the very end of its life, not once per tile.
-    // (descriptors run one tile ahead of the frames they point at)
+    // tiles b, b + grid, ... so the per-workgroup flush happens once per workgroup, at the very
+    // end of its life.  (Per-wave dynamic tile claims from per-XCD-group counters, tried to
+    // even out the workgroups' finishing times, left the spread as it was and cost 2.5 us per
+    // 1M batch: DESIGN.md §8.)  Descriptors run one tile ahead of the frames they point at.
     for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint32_t i = tile * kTile + (uint32_t)tid;
         const bool live = i < a.n;
@@ -931,23 +984,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // frames are 16-byte aligned: the offset in 16-byte units fits one register
         const uint32_t off16 = (uint32_t)(dsc >> 20);
         uint8_t* p = a.frames + ((size_t)off16 << 4);
-
-        // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past
-        // len are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame
-        // costs four loads, not five.  Frames shorter than 49 bytes never take the fast path.
         uint32_t w[20];
-#pragma unroll
-        for (int j = 0; j < 20; ++j) w[j] = 0;
-        if (live) {
-            const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-            for (int c = 0; c < 5; ++c) {
-                if (c < 3 || len > 16u * c) {
-                    const uint4 v = q[c];
-                    w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-                }
-            }
-        }
+        load_window(dsc, live, w);
         {
             const uint32_t nt = tile + gridDim.x;
             dsc_next = 0;
@@ -1004,10 +1042,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const bool slow = live && !fast4 && !fast6;
         if (__any(slow) && slow) {
             Parsed g;
-            if constexpr (kTssMode)
-                general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
-            else
+#if UPE_GP_CALL
+            if constexpr (!kTssMode)
                 general_path_call(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
+            else
+#endif
+                general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
             r = g;
         }
 
@@ -1260,11 +1300,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint32_t cv = 0;   // lane c < C_N: counter c of this workgroup
 #pragma unroll
         for (int v = 0; v < kWaves; ++v) cv += lane < C_N ? s_wv[v][lane] : 0u;
-        if (lane < C_N && cv) atomicAdd(&a.acc_cur->cnt[rep][lane], cv);
-        // the L1 outcome, one atomicMax instruction: minima as kNone - x
-        const uint32_t rv = lane == R_F4 ? kNone - f4 : lane == R_F6 ? kNone - f6
-                          : lane == R_M4 ? x4 : lane == R_M6 ? x6 : kNone - fc;
-        if (lane <= R_CTRL && rv) atomicMax(&a.acc_cur->l1r[rep][lane], rv);
+        if (lane < C_N && cv) atomicAdd(&acc_cur(a)->cnt[rep][lane], cv);
+        // the L1 outcome, one atomicMax instruction: minima as kNone - x, the last table hits
+        // with the workgroup whose payload describes them
+        const unsigned long long rv =
+            lane == R_F4 ? (unsigned long long)(kNone - f4)
+          : lane == R_F6 ? (unsigned long long)(kNone - f6)
+          : lane == R_M4 ? (x4 ? (unsigned long long)x4 << 32 | blockIdx.x : 0ull)
+                         : (x6 ? (unsigned long long)x6 << 32 | blockIdx.x : 0ull);
+        if (lane < R_N && rv) atomicMax(&acc_cur(a)->l1r[rep][lane], rv);
+        if (lane == 0 && fc != kNone) atomicMax(&acc_cur(a)->ctrl[rep], kNone - fc);
         if (lds_stats && small_stats) {
             for (uint32_t k = lane; k < 2 * a.nrules_pad; k += 64) {
                 const uint32_t v = lds_hist[k];
@@ -1275,7 +1320,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // the workgroup's last table hit per family (the next launch reads the one the batch
     // maximum points at)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
-        reinterpret_cast<uint32_t*>(&a.pay[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
+        reinterpret_cast<uint32_t*>(&pay_cur(a)[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
     STAMP(5);
     // Batch k - 1's counters into the cumulative totals (upe_counters_t order): total j by
     // workgroup j % grid (j = 0 the batch size, pkts_in; j >= 1 counter j - 1); one writer per
@@ -1284,8 +1329,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if ((uint32_t)j % gridDim.x != blockIdx.x) continue;
-            const uint32_t v = j == 0 ? *as_const<uint32_t>(&a.acc_prev->n)
-                                      : wave_reduce<0>(lane < kReps ? a.acc_prev->cnt[lane][j - 1]
+            const uint32_t v = j == 0 ? *as_const<uint32_t>(&acc_prev(a)->n)
+                                      : wave_reduce<0>(lane < kReps ? acc_prev(a)->cnt[lane][j - 1]
                                                                     : 0u);
             if (lane == 0 && v) a.st->totals[j] += v;
         }
@@ -1294,18 +1339,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // workgroup 0: the folded starting state for batch k + 1, this batch's grid and size,
         // batch k + 1's accumulators re-armed
         if (lane == 0) {
-            uint4* o = reinterpret_cast<uint4*>(a.l1_out);
+            uint4* o = reinterpret_cast<uint4*>(l1_out(a));
             o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
             o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
             o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
             o[3] = make_uint4(0u, 0u, 0u, 0u);
-            a.acc_cur->grid = gridDim.x;
-            a.acc_cur->n = a.n;
+            acc_cur(a)->grid = gridDim.x;
+            acc_cur(a)->n = a.n;
         }
-        uint32_t* nc = &a.acc_next->cnt[0][0];
-        uint32_t* nr = &a.acc_next->l1r[0][0];
+        uint32_t* nc = &acc_next(a)->cnt[0][0];
+        unsigned long long* nr = &acc_next(a)->l1r[0][0];
         for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
-        for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0u;
+        for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0ull;
+        if (lane < kReps) acc_next(a)->ctrl[lane] = 0u;
     }
 }
 
@@ -1606,6 +1652,7 @@ struct upe_gpu_ctx {
         size_t pk_cap = 0;
         hipEvent_t in_done = nullptr, k_done = nullptr, out_done = nullptr;
         bool busy = false;
+        uint64_t lo = 0, wb = 0;   // host byte range the slot's copy-back writes
     };
     HostSlot hs[3];
 };
@@ -1803,16 +1850,18 @@ uint32_t resident_grid(upe_gpu_ctx* c, bool tss, bool emit, size_t lds, hipStrea
         if (grid > c->paycap) grid = c->paycap;
         Args a;
         memset(&a, 0, sizeof a);
-        a.census = &c->st->census[0];
+        a.census = 1;
+        a.st = c->st;
+        uint32_t* w = &c->st->census[0];
         const uint32_t init[2] = {0u, kNone};
-        if (hipMemcpyAsync(a.census, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) {
+        if (hipMemcpyAsync(w, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) {
             fail("census upload failed");
             return 0;
         }
         launch_classify(tss, emit, grid, lds, s, a);
         uint32_t out[2] = {0u, 0u};
         if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(out, a.census, sizeof out, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(out, w, sizeof out, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
             fail("census launch failed");
             return 0;
@@ -2345,7 +2394,10 @@ int upe_gpu_get_l1(upe_gpu_ctx_t* c, upe_l1_state_t* l1) {
 
 namespace {
 // One batch: the classify launch (in place, or emit mode when d_hdr is given), plus the
-// rule_stats group-by for tables over kLdsStatsMax rules.
+// rule_stats group-by for tables over kLdsStatsMax rules.  A launch takes at most kMaxLaunch
+// packets (the kernel's per-lane counters are 16-bit halves; a lane sees at most one packet
+// per tile).
+constexpr size_t kMaxLaunch = (size_t)1 << 24;
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (!c) return fail("null context");
@@ -2353,6 +2405,18 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
     if (((uintptr_t)d_frames & 15u) != 0) return fail("frames buffer must be 16-byte aligned");
     if (((uintptr_t)d_hdr & 15u) != 0) return fail("header records must be 16-byte aligned");
+    if (n > kMaxLaunch) {
+        // consecutive launches of at most kMaxLaunch packets: the worker's stream semantics are
+        // those of one batch (batch_info describes the last launch)
+        for (size_t s0 = 0; s0 < n; s0 += kMaxLaunch) {
+            const size_t m = n - s0 < kMaxLaunch ? n - s0 : kMaxLaunch;
+            if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
+                             d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
+                             m, stream) != 0)
+                return -1;
+        }
+        return 0;
+    }
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
@@ -2399,13 +2463,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
     a.tss = c->tss ? 1u : 0u;
-    a.pay = pay_slot(c, c->k);
-    a.pay_prev = pay_slot(c, c->k + 1);
-    a.l1_in = l1_slot(c, c->k);
-    a.l1_out = l1_slot(c, c->k + 1);
-    a.acc_cur = acc_slot(c, c->k);
-    a.acc_prev = acc_slot(c, c->k + 2);
-    a.acc_next = acc_slot(c, c->k + 1);
+    a.pay = c->pay;
+    a.paycap = c->paycap;
+    a.k6 = (uint32_t)(c->k % 6);
     a.lb = c->lb;
     a.lb_tag = (uint32_t)(c->k % kLbTagMod) + 1u;
     if (c->k > 0 && c->k % kLbTagMod == 0)   // tags wrap: no flag may carry this launch's tag
@@ -2513,9 +2573,18 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         HIP_TRY(hipStreamSynchronize(c->stream));
         return 0;
     }
-    int rc = 0;
+    // Whatever happens below, no copy into the caller's buffers is left in flight on return.
+    struct Drain {
+        upe_gpu_ctx* c;
+        ~Drain() {
+            (void)hipStreamSynchronize(c->s_in);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->s_out);
+            for (auto& sl : c->hs) sl.busy = false;
+        }
+    } drain{c};
     size_t k = 0;
-    for (size_t s = 0; s < n && rc == 0; s += chunk, ++k) {
+    for (size_t s = 0; s < n; s += chunk, ++k) {
         const size_t e = n - s < chunk ? n : s + chunk, m = e - s;
         // The chunk's byte ranges: [lo, hi) holds every frame's window (the kernel reads up to
         // UPE_FRAME_TAIL bytes from a frame start), [lo, wb) every byte the kernel may rewrite.
@@ -2523,21 +2592,15 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         uint64_t lo = ~0ull, hi = 0, wb = 0;
         for (size_t i = s; i < e; ++i) {
             const uint64_t off = h_desc[i] >> 16, len = h_desc[i] & 0xFFFFu;
-            if (off & 15u) {
-                rc = fail("frame offsets must be multiples of 16 (include/upe_gpu.h)");
-                break;
-            }
+            if (off & 15u) return fail("frame offsets must be multiples of 16 (include/upe_gpu.h)");
             lo = off < lo ? off : lo;
             hi = off + UPE_FRAME_TAIL > hi ? off + UPE_FRAME_TAIL : hi;
             const uint64_t w = off + (len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT);
             wb = w > wb ? w : wb;
         }
-        if (rc) break;
-        if (hi > frames_bytes) {
-            rc = fail("a frame window runs past frames_bytes (UPE_FRAME_TAIL bytes must follow "
-                      "every frame start)");
-            break;
-        }
+        if (hi > frames_bytes)
+            return fail("a frame window runs past frames_bytes (UPE_FRAME_TAIL bytes must follow "
+                        "every frame start)");
         auto& sl = c->hs[k % 3];
         if (sl.busy) HIP_TRY(hipEventSynchronize(sl.out_done));   // the slot's last D2H is done
         sl.busy = false;
@@ -2560,6 +2623,13 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
             HIP_TRY(hipMalloc(&sl.verdict, m * sizeof(uint32_t)));
             sl.pk_cap = m;
         }
+        // A chunk whose bytes interleave with an earlier chunk's (descriptors in any order, e.g.
+        // pool addresses) must read them only after that chunk's copy-back has landed: its own
+        // copy-back rewrites its whole span, and would otherwise put back the earlier chunk's
+        // frames as they were before they were processed.
+        for (auto& other : c->hs)
+            if (&other != &sl && other.busy && other.lo < hi && lo < other.wb)
+                HIP_TRY(hipStreamWaitEvent(c->s_in, other.out_done, 0));
         HIP_TRY(hipMemcpyAsync(sl.frames, h_frames + lo, span, hipMemcpyHostToDevice, c->s_in));
         HIP_TRY(hipMemcpyAsync(sl.desc, h_desc + s, m * sizeof(uint64_t), hipMemcpyHostToDevice,
                                c->s_in));
@@ -2577,10 +2647,11 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
                                c->s_out));
         HIP_TRY(hipEventRecord(sl.out_done, c->s_out));
         sl.busy = true;
+        sl.lo = lo;
+        sl.wb = wb;
     }
     HIP_TRY(hipStreamSynchronize(c->s_out));
-    for (auto& sl : c->hs) sl.busy = false;
-    return rc;
+    return 0;
 }
 
 void* upe_gpu_host_alloc(size_t bytes) {
@@ -2778,7 +2849,9 @@ int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_
                 wrote = true;
             }
         } else {
-            // NS / NA option walk, src/worker.c:64-95, over the whole frame when it is long
+            // NS / NA option walk, src/worker.c:64-95, over the whole frame when it is long.
+            // This reads len bytes at the frame start: the call takes full frames only
+            // (include/upe_gpu.h), never the UPE_FRAME_TAIL-byte header windows of the host path.
             const uint8_t* f = b;
             if (len > kCtrlWin) {
                 uint64_t d = 0;
@@ -2839,7 +2912,7 @@ int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
     for (int r = 0; r < kReps; ++r) {
         for (int j = 0; j < 7; ++j) dst[1 + j] += b.cnt[r][j];
         info->n_ctrl += b.cnt[r][C_CTRL];
-        cm = std::max(cm, b.l1r[r][R_CTRL]);
+        cm = std::max(cm, b.ctrl[r]);
     }
     if (cm) info->first_ctrl = kNone - cm;
     return 0;
