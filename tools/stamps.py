@@ -26,21 +26,38 @@ names = ["entry", "init", "win", "scan", "loop", "flush", "wait", "ticket", "tai
 for rep in range(6):
     buf = np.zeros(8192 * 16, np.uint64)
     lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), 0)  # no-op read
-    if emit:
-        w.process_emit(frames[rep], desc, verdict, hdr, n)
-    else:
-        w.process(frames[rep], desc, verdict, n)
+    # the last of 4 back-to-back launches (as the bench queues them), not an isolated one
+    for k in range(4):
+        f = frames[(rep + k) % len(frames)]
+        if emit:
+            w.process_emit(f, desc, verdict, hdr, n)
+        else:
+            w.process(f, desc, verdict, n)
     w.sync()
     lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes)
-    ntiles = (n + 255) // 256
-    grid = min(ntiles, 8192)
-    st = buf.reshape(8192, 16)[:grid, :11].astype(np.int64)
+    # stamps of launch k sit in slot k % 4 (2048 workgroup rows each)
+    slots = buf.reshape(4, 2048, 16).astype(np.int64)
+    spans = []
+    for sl in range(4):
+        e = slots[sl, :, 0]
+        ok = e > 0
+        if ok.any():
+            spans.append((e[ok].min(), slots[sl, ok, 5].max(), sl))
+    spans.sort()
+    if len(spans) > 1:
+        gaps = [(spans[j + 1][0] - spans[j][1]) / 100.0 for j in range(len(spans) - 1)]
+        lens = [(b - a) / 100.0 for a, b, _ in spans]
+        print(f"rep {rep}: launch spans (first entry -> last flush) {np.round(lens, 2).tolist()} us; "
+              f"gaps (last flush -> next first entry) {np.round(gaps, 2).tolist()} us")
+    raw = slots[spans[-1][2]]
+    st = raw[:, :11]
     valid = st[:, 0] > 0
     st = st[valid]
+    xcc = raw[valid, 11]
+    hw = raw[valid, 12]
     t0 = st[:, 0].min()
     rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
-    print(f"rep {rep}: grid {st.shape[0]} WGs; end of kernel ~{rel[:, 7].max():.2f} us; tail end "
-          f"{rel[:, 8].max():.2f} us")
+    print(f"rep {rep}: grid {st.shape[0]} WGs; last flush {rel[:, 5].max():.2f} us")
     if rep == 5:
         # where the loop-end spread comes from: by blockIdx % 8 (the XCD group) and by start time
         loop = rel[:, 4]
@@ -56,6 +73,23 @@ for rep in range(6):
             print(f"   entry quartile {k}: entry {np.median(ent[idx]):5.2f} loop end med "
                   f"{np.median(loop[idx]):6.2f} max {loop[idx].max():6.2f}")
         print("   corr(entry, loop end) =", round(float(np.corrcoef(ent, loop)[0, 1]), 3))
+        # by the XCC the workgroup really ran on (HW_REG_XCC_ID), and by CU within it
+        cu = (xcc << 8) | (((hw >> 13) & 7) << 4) | ((hw >> 8) & 15)
+        for g in range(8):
+            sel = xcc == g
+            if sel.any():
+                print(f"   XCC {g}: {sel.sum():4d} WGs on {np.unique(cu[sel]).size:3d} CUs; entry med "
+                      f"{np.median(ent[sel]):5.2f} max {ent[sel].max():5.2f}; loop end med "
+                      f"{np.median(loop[sel]):6.2f} max {loop[sel].max():6.2f}; blockIdx%8 "
+                      f"{np.unique(b[sel] % 8).tolist()}")
+        ucu, cnt = np.unique(cu, return_counts=True)
+        print("   WGs per CU:", dict(zip(*np.unique(cnt, return_counts=True))))
+        cu_end = {c: loop[cu == c].max() for c in ucu}
+        worst = sorted(cu_end, key=cu_end.get)[-6:]
+        for c in worst:
+            sel = cu == c
+            print(f"   slow CU xcc{c >> 8} se{(c >> 4) & 15} cu{c & 15}: loop ends "
+                  f"{np.round(np.sort(loop[sel]), 2).tolist()} entries {np.round(np.sort(ent[sel]), 2).tolist()}")
         last = np.argsort(loop)[-10:]
         print("   10 latest loop ends: blocks", b[last].tolist(), "entry", np.round(ent[last], 2).tolist())
     for j, nm in enumerate(names):

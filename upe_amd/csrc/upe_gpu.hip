@@ -66,11 +66,18 @@
 namespace {
 
 #ifndef UPE_BLOCK
-#define UPE_BLOCK 256
+#define UPE_BLOCK 1024
 #endif
 constexpr int kBlock = UPE_BLOCK;      // threads per workgroup = packets per tile
-constexpr int kWaves = kBlock / 64;
+constexpr int kWaves = kBlock / 64;    // 64-packet chunks per tile
 constexpr int kTile = kBlock;
+// Output stores (verdicts, records): plain (0), nontemporal (1), nontemporal in each
+// workgroup's last chunks (2).
+#ifndef UPE_NT_OUT
+#define UPE_NT_OUT 0
+#endif
+constexpr int kNtOut = UPE_NT_OUT;
+
 #ifndef UPE_WAVES_PER_SIMD
 #define UPE_WAVES_PER_SIMD 4
 #endif
@@ -267,7 +274,7 @@ __device__ unsigned long long g_stamps[8192 * 16];
         if (threadIdx.x == 0) {                                                               \
             unsigned long long t_;                                                            \
             asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
-            g_stamps[blockIdx.x * 16 + (k)] = t_;                                             \
+            g_stamps[(blockIdx.x + ((a.lb_tag - 1u) % 4u) * 2048u) * 16 + (k)] = t_;                                             \
         }                                                                                     \
     } while (0)
 #define STAMP_VM(k)                                                                           \
@@ -275,7 +282,19 @@ __device__ unsigned long long g_stamps[8192 * 16];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
         STAMP(k);                                                                             \
     } while (0)
+// where the workgroup runs: slot 11 = XCC id, slot 12 = HW_ID (CU, SE, ...)
+#define STAMP_WHERE()                                                                         \
+    do {                                                                                      \
+        if (threadIdx.x == 0) {                                                               \
+            uint32_t x_, h_;                                                                  \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x_));                 \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h_));                  \
+            g_stamps[(blockIdx.x + ((a.lb_tag - 1u) % 4u) * 2048u) * 16 + 11] = x_;                                              \
+            g_stamps[(blockIdx.x + ((a.lb_tag - 1u) % 4u) * 2048u) * 16 + 12] = h_;                                              \
+        }                                                                                     \
+    } while (0)
 #else
+#define STAMP_WHERE() do {} while (0)
 #define STAMP(k) do {} while (0)
 #define STAMP_VM(k) do {} while (0)
 #endif
@@ -878,11 +897,12 @@ template <bool kTssMode, bool kEmit>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
-    __shared__ uint32_t s_wv[kWaves][13];
-    __shared__ uint32_t s_pay[kWaves][kPayWords];
-    __shared__ uint32_t s_lpay[kBlock][kPayWords];   // each lane's latest table hit
+    __shared__ uint32_t s_tot[C_N + 3];   // the workgroup's counters; first f4 / f6 / ctrl (min)
+    __shared__ uint32_t s_wm[kWaves][2];  // per wave: its last table hit per family (index + 1)
+    __shared__ uint32_t s_pay[kWaves][kPayWords];   // ... and that hit's (ip, MAC)
     __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
+    __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -890,6 +910,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     }
     if (kAblate & 64) return;
     STAMP(0);
+    STAMP_WHERE();
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -917,12 +938,27 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
         }
     };
+    // Work: the workgroup owns tiles blockIdx, blockIdx + grid, ... (one per CU at a time, so a
+    // CU's tiles are one workgroup's), and each wave takes 64-packet chunks of them in order:
+    // workgroup-local chunk k is chunk k % kWaves of the workgroup's tile k / kWaves.  Waves
+    // claim k from an LDS counter, so the workgroup's waves finish together however unevenly
+    // the CU schedules them (with several workgroups per CU and static tiles, the last one to
+    // finish ran alone for ~4 us after the first: the CU favours older waves).  Global chunk
+    // numbers ascend with k, and a wave's claims ascend.
+    auto chunk_of = [&](uint32_t k) -> uint32_t {
+        const uint32_t t = blockIdx.x + (k / (uint32_t)kWaves) * gridDim.x;
+        const uint32_t c = t * (uint32_t)kWaves + k % (uint32_t)kWaves;
+        return t < a.ntiles && c * 64u < a.n ? c : kNone;
+    };
+    if (tid == 0) s_claim = kWaves;
+    if (tid < C_N + 3) s_tot[tid] = tid < C_N ? 0u : kNone;
+    if (tid < 2 * kWaves) s_wm[tid / 2][tid % 2] = 0u;
+    uint32_t kc = (uint32_t)wave, ch = chunk_of(kc);   // workgroup-local index, chunk
     // The first descriptor (its round trip runs under the table staging below), then small
     // rule tables into LDS, before the entry barrier.  (Issuing the first tile's window loads
     // here too made the staging wait for them at the barrier: 2.5 us per 1M batch slower.)
     uint64_t dsc_next = 0;
-    if (blockIdx.x < a.ntiles && blockIdx.x * kTile + (uint32_t)tid < a.n)
-        dsc_next = a.desc[blockIdx.x * kTile + (uint32_t)tid];
+    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[ch * 64u + lane];
     if (!kTssMode && small_stats) {
         const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
         const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
@@ -951,6 +987,36 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // off the path to the first frames.
     uint32_t L1[11];
     bool look4 = false, look6 = false, folded = false;
+    // Bookkeeping between batches, done by wave 0 of workgroups 0..7 before its first chunk (so
+    // that it is off the end of the launch: their other waves take more chunks meanwhile).
+    // Nothing else in this launch touches what it writes.
+    auto books = [&]() {
+        // batch k - 1's counters into the cumulative totals (upe_counters_t order): total j by
+        // workgroup j % grid (j = 0 the batch size, pkts_in; j >= 1 counter j - 1)
+        if (blockIdx.x < 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if ((uint32_t)j % gridDim.x != blockIdx.x) continue;
+                const uint32_t v = j == 0 ? *as_const<uint32_t>(&acc_prev(a)->n)
+                                          : wave_reduce<0>(lane < kReps ? acc_prev(a)->cnt[lane][j - 1]
+                                                                        : 0u);
+                if (lane == 0 && v) a.st->totals[j] += v;
+            }
+        }
+        if (blockIdx.x == 0) {
+            // workgroup 0: this batch's grid and size, batch k + 1's accumulators re-armed
+            // (batch k - 2's, folded by batch k - 1)
+            if (lane == 0) {
+                acc_cur(a)->grid = gridDim.x;
+                acc_cur(a)->n = a.n;
+            }
+            uint32_t* nc = &acc_next(a)->cnt[0][0];
+            unsigned long long* nr = &acc_next(a)->l1r[0][0];
+            for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
+            for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0ull;
+            if (lane < kReps) acc_next(a)->ctrl[lane] = 0u;
+        }
+    };
     auto fold_start = [&]() {
         if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
 #pragma unroll
@@ -963,21 +1029,25 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
         folded = true;
     };
+    if (wave == 0 && blockIdx.x < 8) books();
 
-    // Per-lane accumulators over this workgroup's tiles, reduced once at the end (not per tile):
-    // counters as 16-bit pairs (a lane sees at most one packet per tile, and a workgroup takes
-    // fewer than 2^16 tiles), first / last packet indexes of the L1 bookkeeping as running
-    // min / max; each lane's latest table hit is kept in LDS (tiles ascend, so it is the
-    // lane's last one).
-    uint32_t c01 = 0, c23 = 0, c45 = 0, c67 = 0;
-    uint32_t lf4 = kNone, lf6 = kNone, lfc = kNone, lm4 = 0, lm6 = 0;
-    // Persistent workgroups: the grid is what the chip holds at once, and workgroup b takes
-    // tiles b, b + grid, ... so the per-workgroup flush happens once per workgroup, at the very
-    // end of its life.  (Per-wave dynamic tile claims from per-XCD-group counters, tried to
-    // even out the workgroups' finishing times, left the spread as it was and cost 2.5 us per
-    // 1M batch: DESIGN.md §8.)  Descriptors run one tile ahead of the frames they point at.
-    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-        const uint32_t i = tile * kTile + (uint32_t)tid;
+    // Persistent workgroups: the grid is what the chip holds at once, so the per-workgroup
+    // flush happens once per workgroup, at the very end of its life.  (Per-wave claims from
+    // device-scope counters shared by many workgroups cost 2.5 us per 1M batch: every claim
+    // serialised on a few hot lines; the LDS counter is private to the workgroup.)
+    // Descriptors run one chunk ahead of the frames they point at.
+    uint32_t kcn = 0, chn = kNone;   // this wave's next chunk
+    for (bool first = true; ch != kNone; first = false, ch = chn, kc = kcn) {
+        {
+            uint32_t kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_claim, 1u);
+            kcn = __builtin_amdgcn_readfirstlane(kn);
+            chn = chunk_of(kcn);
+        }
+        // nontemporal output stores: everywhere (1), or in the workgroup's last two rounds of
+        // chunks (2), whose lines would otherwise still be dirty in L2 when the launch ends
+        const bool nt = kNtOut == 1 || (kNtOut == 2 && chunk_of(kc + 2u * kWaves) == kNone);
+        const uint32_t i = ch * 64u + (uint32_t)lane;
         const bool live = i < a.n;
         const uint64_t dsc = dsc_next;
         const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
@@ -986,14 +1056,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint8_t* p = a.frames + ((size_t)off16 << 4);
         uint32_t w[20];
         load_window(dsc, live, w);
-        {
-            const uint32_t nt = tile + gridDim.x;
-            dsc_next = 0;
-            if (nt < a.ntiles && nt * kTile + (uint32_t)tid < a.n) dsc_next = a.desc[nt * kTile + tid];
-        }
+        dsc_next = 0;
+        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
         if (!folded) fold_start();
 
-        if (tile == blockIdx.x) STAMP_VM(2);
+        if (first) STAMP_VM(2);
         // ---- fast path: option-less IPv4 / IPv6 ----
         const uint32_t e12 = w[3] & 0xFFFFu;          // bytes 12,13 (ethertype, byte-swapped)
         const bool fast4 = live && len >= 34u && e12 == 0x0008u && byte_of(w[3], 2) == 0x45u;
@@ -1107,7 +1174,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             code = ac == 0u ? UPE_V_DROP_RULE : ac == 1u ? UPE_V_FWD : UPE_V_DROP_ACTION;
         }
         uint32_t flags = r.flags;
-        if (tile == blockIdx.x) STAMP_VM(3);
+        if (first) STAMP_VM(3);
 
         // ---- L3 forward (src/worker.c:155-244) ----
         bool fp4 = false, fp6 = false;       // this packet misses the start entry, hits table
@@ -1138,7 +1205,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             // The starting entry disagrees with the table: publish this chunk's miss-then-hit
             // packets, and give the packets aimed at the entry the entry's MAC unless an earlier
             // packet of their family missed it and hit the table (lookback).
-            const uint32_t chunk = tile * kWaves + (uint32_t)wave;
+            const uint32_t chunk = ch;
             const unsigned long long b4 = __ballot(fp4), b6 = __ballot(fp6);
             const uint32_t fpb = (b4 ? (uint32_t)LB_FP4 : 0u) | (b6 ? (uint32_t)LB_FP6 : 0u);
             const uint32_t tag = a.lb_tag << 6;
@@ -1184,7 +1251,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
                              : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
             }
-            a.hdr[i] = rec;
+            if (nt) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 v = {rec.x, rec.y, rec.z, rec.w};
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(&a.hdr[i]));
+            } else {
+                a.hdr[i] = rec;
+            }
         } else if (live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
@@ -1192,7 +1265,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                           (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
-        if (live) a.verdict[i] = code | flags | rbits;
+        if (live) {
+            if (nt) __builtin_nontemporal_store(code | flags | rbits, &a.verdict[i]);
+            else a.verdict[i] = code | flags | rbits;
+        }
         if (a.lens16 && live) a.lens16[i] = (uint16_t)len;   // 2 B/packet for upe_rule_hist
         if (a.flow_hash && live) {
             // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
@@ -1211,57 +1287,42 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             atomicAdd(reinterpret_cast<unsigned long long*>(&lds_hist[2 * ri]),
                       ((unsigned long long)len << 32) | 1ull);
 
-        // ---- per-lane totals and L1 bookkeeping ----
-        c01 += (ok ? 1u : 0u) + (ok && ri != kNone ? 0x10000u : 0u);
-        c23 += (live && code == UPE_V_FWD ? 1u : 0u) +
-               (live && code != UPE_V_FWD && code != UPE_V_CONSUMED ? 0x10000u : 0u);
-        c45 += (live && r.consumed ? 1u : 0u) +
-               (live && !r.consumed && (r.flags & UPE_VF_ARP_LEARN) ? 0x10000u : 0u);
-        c67 += (live && !r.consumed && (r.flags & UPE_VF_ARP_REPLY) ? 1u : 0u) +
-               (ctrl ? 0x10000u : 0u);
-        lf4 = min(lf4, fp4 ? i : kNone);
-        lf6 = min(lf6, fp6 ? i : kNone);
-        lfc = min(lfc, ctrl ? i : kNone);
-        lm4 = max(lm4, thit4 ? i + 1 : 0u);
-        lm6 = max(lm6, thit6 ? i + 1 : 0u);
-        if (thit4) {
-            s_lpay[tid][0] = r.d[0]; s_lpay[tid][1] = mlo; s_lpay[tid][2] = mhi;
-        }
-        if (thit6) {
-            s_lpay[tid][3] = r.d[0]; s_lpay[tid][4] = r.d[1]; s_lpay[tid][5] = r.d[2];
-            s_lpay[tid][6] = r.d[3]; s_lpay[tid][7] = mlo; s_lpay[tid][8] = mhi;
+        // ---- counters and L1 bookkeeping: ballots, added by one lane into the workgroup's LDS
+        // totals (no per-lane accumulators to reduce at the end).  A wave's chunks ascend, so its
+        // latest table hit per family is the highest such lane of its latest chunk with one, and
+        // that lane leaves the hit's payload in the wave's slot. ----
+        {
+            const bool nc = live && !r.consumed;
+            const unsigned long long bm[C_N] = {
+                __ballot(ok), __ballot(ok && ri != kNone), __ballot(live && code == UPE_V_FWD),
+                __ballot(live && code != UPE_V_FWD && code != UPE_V_CONSUMED),
+                __ballot(live && r.consumed), __ballot(nc && (r.flags & UPE_VF_ARP_LEARN)),
+                __ballot(nc && (r.flags & UPE_VF_ARP_REPLY)), __ballot(ctrl)};
+            const unsigned long long q4 = __ballot(fp4), q6 = __ballot(fp6);
+            const unsigned long long h4 = __ballot(thit4), h6 = __ballot(thit6);
+            const uint32_t base = ch * 64u;
+            if (lane == 0) {
+#pragma unroll
+                for (int c = 0; c < C_N; ++c)
+                    if (bm[c]) atomicAdd(&s_tot[c], (uint32_t)__popcll(bm[c]));
+                if (q4) atomicMin(&s_tot[C_N + 0], base + (uint32_t)__builtin_ctzll(q4));
+                if (q6) atomicMin(&s_tot[C_N + 1], base + (uint32_t)__builtin_ctzll(q6));
+                if (bm[C_CTRL])
+                    atomicMin(&s_tot[C_N + 2], base + (uint32_t)__builtin_ctzll(bm[C_CTRL]));
+                if (h4) s_wm[wave][0] = base + 64u - (uint32_t)__builtin_clzll(h4);   // index + 1
+                if (h6) s_wm[wave][1] = base + 64u - (uint32_t)__builtin_clzll(h6);
+            }
+            if (h4 && lane == 63 - __builtin_clzll(h4)) {
+                s_pay[wave][0] = r.d[0]; s_pay[wave][1] = mlo; s_pay[wave][2] = mhi;
+            }
+            if (h6 && lane == 63 - __builtin_clzll(h6)) {
+                s_pay[wave][3] = r.d[0]; s_pay[wave][4] = r.d[1]; s_pay[wave][5] = r.d[2];
+                s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
+            }
         }
     }
     STAMP(4);
     if (!folded) fold_start();
-    // ---- reduce the per-lane accumulators: DPP rotations inside each 16-lane row, then the four
-    // row results through scalar registers; then across the workgroup's waves in LDS ----
-    {
-        const uint32_t cs[8] = {c01 & 0xFFFFu, c01 >> 16, c23 & 0xFFFFu, c23 >> 16,
-                                c45 & 0xFFFFu, c45 >> 16, c67 & 0xFFFFu, c67 >> 16};
-        const int w = wave;
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) s_wv[w][c] = 0;
-        }
-        uint32_t v[13];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = wave_reduce<0>(cs[c]);
-        v[8] = wave_reduce<1>(lf4);
-        v[9] = wave_reduce<1>(lf6);
-        v[10] = wave_reduce<1>(lfc);
-        v[11] = wave_reduce<2>(lm4);
-        v[12] = wave_reduce<2>(lm6);
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < 13; ++c) s_wv[w][c] = v[c];
-        }
-        // the lane holding the wave's last table hit per family hands over its payload
-        if (v[11] && lm4 == v[11])
-            for (int j = 0; j < 3; ++j) s_pay[w][j] = s_lpay[tid][j];
-        if (v[12] && lm6 == v[12])
-            for (int j = 3; j < kPayWords; ++j) s_pay[w][j] = s_lpay[tid][j];
-    }
     STAMP(9);
     // A bare barrier: LDS drained (lgkmcnt), global stores left in flight (nothing in this launch
     // reads what this workgroup wrote; __syncthreads() would make every wave wait for its write
@@ -1286,20 +1347,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // waits for them: the next launch reads them (kernel boundary), the host after a
     // synchronisation.
     const uint32_t rep = blockIdx.x % kReps;
-    uint32_t x4 = 0, x6 = 0, f4 = kNone, f6 = kNone, fc = kNone;
-    int w4 = 0, w6 = 0;
-#pragma unroll
-    for (int v = 0; v < kWaves; ++v) {
-        if (s_wv[v][11] > x4) { x4 = s_wv[v][11]; w4 = v; }
-        if (s_wv[v][12] > x6) { x6 = s_wv[v][12]; w6 = v; }
-        f4 = min(f4, s_wv[v][8]);
-        f6 = min(f6, s_wv[v][9]);
-        fc = min(fc, s_wv[v][10]);
-    }
+    const uint32_t f4 = s_tot[C_N + 0], f6 = s_tot[C_N + 1], fc = s_tot[C_N + 2];
+    // the workgroup's last table hit per family and the wave holding its payload: lane v reads
+    // wave v's (index + 1) << 4 | v, and the maximum names both (index + 1 < 2^25)
+    static_assert(kWaves <= 16, "the wave index is packed in 4 bits");
+    const uint32_t m4 = wave_reduce<2>(lane < kWaves ? s_wm[lane][0] << 4 | (uint32_t)lane : 0u);
+    const uint32_t m6 = wave_reduce<2>(lane < kWaves ? s_wm[lane][1] << 4 | (uint32_t)lane : 0u);
+    const uint32_t x4 = m4 >> 4, x6 = m6 >> 4;
+    const int w4 = (int)(m4 & 15u), w6 = (int)(m6 & 15u);
     if (!(kAblate & 4)) {
-        uint32_t cv = 0;   // lane c < C_N: counter c of this workgroup
-#pragma unroll
-        for (int v = 0; v < kWaves; ++v) cv += lane < C_N ? s_wv[v][lane] : 0u;
+        const uint32_t cv = lane < C_N ? s_tot[lane] : 0u;   // lane c < C_N: counter c
         if (lane < C_N && cv) atomicAdd(&acc_cur(a)->cnt[rep][lane], cv);
         // the L1 outcome, one atomicMax instruction: minima as kNone - x, the last table hits
         // with the workgroup whose payload describes them
@@ -1321,38 +1378,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // maximum points at)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
         reinterpret_cast<uint32_t*>(&pay_cur(a)[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
+    // workgroup 0: the folded starting state for batch k + 1 (which folds this batch's outcome
+    // into it)
+    if (blockIdx.x == 0 && lane == 0) {
+        uint4* o = reinterpret_cast<uint4*>(l1_out(a));
+        o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
+        o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
+        o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
+        o[3] = make_uint4(0u, 0u, 0u, 0u);
+    }
     STAMP(5);
-    // Batch k - 1's counters into the cumulative totals (upe_counters_t order): total j by
-    // workgroup j % grid (j = 0 the batch size, pkts_in; j >= 1 counter j - 1); one writer per
-    // word, nobody else reads them in this launch.
-    if (blockIdx.x < 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if ((uint32_t)j % gridDim.x != blockIdx.x) continue;
-            const uint32_t v = j == 0 ? *as_const<uint32_t>(&acc_prev(a)->n)
-                                      : wave_reduce<0>(lane < kReps ? acc_prev(a)->cnt[lane][j - 1]
-                                                                    : 0u);
-            if (lane == 0 && v) a.st->totals[j] += v;
-        }
-    }
-    if (blockIdx.x == 0) {
-        // workgroup 0: the folded starting state for batch k + 1, this batch's grid and size,
-        // batch k + 1's accumulators re-armed
-        if (lane == 0) {
-            uint4* o = reinterpret_cast<uint4*>(l1_out(a));
-            o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
-            o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
-            o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
-            o[3] = make_uint4(0u, 0u, 0u, 0u);
-            acc_cur(a)->grid = gridDim.x;
-            acc_cur(a)->n = a.n;
-        }
-        uint32_t* nc = &acc_next(a)->cnt[0][0];
-        unsigned long long* nr = &acc_next(a)->l1r[0][0];
-        for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
-        for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0ull;
-        if (lane < kReps) acc_next(a)->ctrl[lane] = 0u;
-    }
 }
 
 
