@@ -1,5 +1,5 @@
 """Diagnostic: per-workgroup phase timestamps of one upe_classify launch (UPE_STAMPS build).
-Usage: UPE_GPU_LIB_DIAG=build/diag/libupe_gpu_stamps.so python tools/stamps.py [packets]"""
+Usage: UPE_GPU_LIB_DIAG=build/var/stamps.so python tools/stamps.py [packets] [emit|inplace] [B|C]"""
 import ctypes
 import os
 import sys
@@ -12,7 +12,8 @@ from upe_amd import gpu, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 emit = (sys.argv[2] if len(sys.argv) > 2 else "emit") == "emit"
-wl = synth.config_b(n=n)
+cfg = sys.argv[3] if len(sys.argv) > 3 else "B"
+wl = {"B": synth.config_b, "C": synth.config_c}[cfg](n=n)
 w = gpu.GpuWorker(0, wl.capacity)
 w.configure(wl)
 dev = torch.device("cuda", 0)

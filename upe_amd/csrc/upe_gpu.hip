@@ -57,6 +57,7 @@
 #include <algorithm>
 #include <array>
 #include <map>
+#include <atomic>
 #include <new>
 #include <string>
 #include <vector>
@@ -89,10 +90,17 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
+// Neighbour indexes staged in LDS (one workgroup per CU, so a CU reads them once per launch):
+// ARP up to 2048 slots (32 KB), NDP up to 2048 slots (64 KB), within kLdsDynMax of dynamic LDS.
 #ifndef UPE_ARP_LDS_SLOTS
-#define UPE_ARP_LDS_SLOTS 1024
+#define UPE_ARP_LDS_SLOTS 2048
 #endif
-constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;   // ARP indexes up to 16 KB are staged in LDS
+#ifndef UPE_NDP_LDS_SLOTS
+#define UPE_NDP_LDS_SLOTS 2048
+#endif
+constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;
+constexpr uint32_t kNdpLdsSlots = UPE_NDP_LDS_SLOTS;
+constexpr size_t kLdsDynMax = 136 * 1024;
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 #ifndef UPE_ABLATE
@@ -239,6 +247,7 @@ struct Args {
     unsigned long long* stats;       // [cap][2]
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
+    uint32_t ndp_lds;                // NDP index staged in LDS (slots, 2 x uint4 each), 0 = not
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
     uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
@@ -374,6 +383,20 @@ __device__ __forceinline__ bool arp_lookup_lds(const uint4* t, uint32_t bits, ui
     const bool h2 = ((e2.z >> 16) & 1u) && e2.x == ip;
     lo = h1 ? e1.y : e2.y;
     hi = (h1 ? e1.z : e2.z) & 0xFFFFu;
+    return h1 || h2;
+}
+__device__ __forceinline__ bool ndp_lookup_lds(const uint4* t, uint32_t bits, uint32_t seed,
+                                               const uint32_t ip[4], uint32_t& lo, uint32_t& hi) {
+    const uint32_t k = fold_v6(ip);
+    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits);
+    const uint4 a1 = t[2 * t1], m1 = t[2 * t1 + 1];
+    const uint4 a2 = t[2 * t2], m2 = t[2 * t2 + 1];
+    const bool h1 = ((m1.y >> 16) & 1u) && a1.x == ip[0] && a1.y == ip[1] && a1.z == ip[2] &&
+                    a1.w == ip[3];
+    const bool h2 = ((m2.y >> 16) & 1u) && a2.x == ip[0] && a2.y == ip[1] && a2.z == ip[2] &&
+                    a2.w == ip[3];
+    lo = h1 ? m1.x : m2.x;
+    hi = (h1 ? m1.y : m2.y) & 0xFFFFu;
     return h1 || h2;
 }
 __device__ __forceinline__ bool ndp_lookup(const NeighIndex& x, const uint32_t ip[4], uint32_t& lo,
@@ -955,8 +978,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (tid < 2 * kWaves) s_wm[tid / 2][tid % 2] = 0u;
     uint32_t kc = (uint32_t)wave, ch = chunk_of(kc);   // workgroup-local index, chunk
     // The first descriptor (its round trip runs under the table staging below), then small
-    // rule tables into LDS, before the entry barrier.  (Issuing the first tile's window loads
-    // here too made the staging wait for them at the barrier: 2.5 us per 1M batch slower.)
+    // rule tables into LDS, before the entry barrier.  (Issuing the first chunk's window loads
+    // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
     uint64_t dsc_next = 0;
     if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[ch * 64u + lane];
     if (!kTssMode && small_stats) {
@@ -975,11 +998,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     unsigned long long pr[R_N] = {0, 0, 0, 0};
     if (lane < kReps)
         for (int j = 0; j < R_N; ++j) pr[j] = acc_prev(a)->l1r[lane][j];
-    // small ARP indexes (<= 16 KB) into LDS after the rule-stats bins: a lookup is then an LDS
-    // read, not a memory round trip queued behind the batch's frame traffic
+    // small neighbour indexes into LDS after the rule-stats bins: a lookup is then an LDS read,
+    // not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
-    if (a.arp_lds)
-        for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
+    uint4* s_ndp = s_arp + a.arp_lds;
+    for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
+    for (uint32_t k = tid; k < 2 * a.ndp_lds; k += kBlock) s_ndp[k] = a.ndp.t[k];
     __syncthreads();
     STAMP(1);
     // The fold itself waits on those loads (and then on at most two payload loads), so it runs
@@ -1128,6 +1152,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (ok && r.ttl > 1u && !(kAblate & 2)) {
             if (!r.v6 && a.arp_lds)
                 nhit = arp_lookup_lds(s_arp, a.arp.bits, a.arp.seed, r.d[0], mlo, mhi);
+            else if (r.v6 && a.ndp_lds)
+                nhit = ndp_lookup_lds(s_ndp, a.ndp.bits, a.ndp.seed, r.d, mlo, mhi);
             else
                 nhit = neigh_lookup(a.arp, a.ndp, r.v6, r.d, mlo, mhi);
         }
@@ -1847,6 +1873,21 @@ int check_lookback(upe_gpu_ctx* c) {
 }
 
 void launch_classify(bool tss, bool emit, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
+    // dynamic LDS beyond 64 KB must be allowed per kernel and device (once per device)
+    static std::atomic<uint64_t> lds_attr{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(lds_attr.fetch_or(bit) & bit)) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+    }
     if (tss && emit)
         hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a);
     else if (tss)
@@ -2527,8 +2568,17 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
     // array 16-byte aligned after the bins)
     const uint32_t arp_slots = c->arp_bits ? (1u << c->arp_bits) : 0u;
-    a.arp_lds = (arp_slots && arp_slots <= kArpLdsSlots && hist <= 8192) ? arp_slots : 0u;
-    const size_t lds = hist + (size_t)a.arp_lds * sizeof(uint4);
+    const uint32_t ndp_slots = c->ndp_bits ? (1u << c->ndp_bits) : 0u;
+    size_t lds = hist;
+    a.arp_lds = a.ndp_lds = 0u;
+    if (arp_slots && arp_slots <= kArpLdsSlots && lds + arp_slots * sizeof(uint4) <= kLdsDynMax) {
+        a.arp_lds = arp_slots;
+        lds += arp_slots * sizeof(uint4);
+    }
+    if (ndp_slots && ndp_slots <= kNdpLdsSlots && lds + 2 * ndp_slots * sizeof(uint4) <= kLdsDynMax) {
+        a.ndp_lds = ndp_slots;
+        lds += 2 * ndp_slots * sizeof(uint4);
+    }
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, c->tss, emit, lds, s);
     if (grid_cap == 0) return -1;
