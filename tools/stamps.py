@@ -23,7 +23,7 @@ verdict = torch.empty(n, dtype=torch.int32, device=dev)
 hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 lib = gpu.LIB
 lib.upe_gpu_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-names = ["entry", "init", "win", "scan", "loop", "flush", "wait", "ticket", "tail", "reduced", "barrier"]
+names = ["entry", "init", "win", "scan", "loop", "flush", "-", "-", "-", "reduced", "barrier"]
 for rep in range(6):
     buf = np.zeros(8192 * 16, np.uint64)
     lib.upe_gpu_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), 0)  # no-op read
@@ -94,9 +94,9 @@ for rep in range(6):
         last = np.argsort(loop)[-10:]
         print("   10 latest loop ends: blocks", b[last].tolist(), "entry", np.round(ent[last], 2).tolist())
     for j, nm in enumerate(names):
+        if nm == "-":
+            continue
         col = rel[:, j]
         col = col[col >= 0]
-        if j == 8:
-            col = rel[:, 8][st[:, 8] > 0]
         if col.size:
             print(f"   {nm:7s} min {col.min():7.2f} med {np.median(col):7.2f} max {col.max():7.2f}")

@@ -7,13 +7,14 @@
 // (src/rule_table.c:76-91,163-176), counters and rule_stats (src/worker.c:119-153), and the
 // L3-forward rewrite: TTL / hop-limit decrement, RFC 1071 checksum (src/parser.c:137-169), and the
 // next-hop MAC that arp_get_mac / ndp_get_mac would return (src/arp_table.c:55-80,
-// src/ndp_table.c:6-17,67-86).  Frames are rewritten in place in HBM.
+// src/ndp_table.c:6-17,67-86).  The rewritten header bytes go either to a 16-byte record per
+// packet (emit mode, frames only read) or into the frames in place.
 //
-// Data layout (DESIGN.md "HBM layout"): frames packed back to back at 16-byte aligned starts,
-// one uint64 descriptor per packet (offset << 16 | len), one uint32 verdict per packet.  A lane
-// loads the first 80 bytes of its frame as five 16-byte vector loads, issued together (the batch
-// buffer carries a 96-byte tail, so the last frame's window is readable); frames are 16-byte
-// aligned, so the loads never split a frame's line between two requests more than necessary.
+// Data layout: frames packed back to back at 16-byte aligned starts, one uint64
+// descriptor per packet (offset << 16 | len), one uint32 verdict per packet, and in emit mode one
+// upe_hdr_rec_t per packet.  A lane loads the first 80 bytes of its frame as 16-byte vector
+// loads issued together (chunks past len are not loaded; the batch buffer carries a 96-byte
+// tail, so the last frame's window is readable).
 //
 // Fast path: option-less IPv4 (first byte 0x45, len >= 34) and IPv6 (len >= 54), which covers
 // every well-formed packet of the benchmark configurations, is parsed branch-free from those
@@ -21,22 +22,25 @@
 // path, entered only by waves that hold such a packet.
 //
 // The rule table is compiled into structure-of-arrays streams that a wave scans with
-// wave-uniform (scalar-unit) loads, so rule operands arrive in SGPRs; the per-rule work is a few
-// VALU xor / and-or against them, with an early exit as soon as every lane of the wave has its
-// first match (ballot).
+// wave-uniform loads (LDS for small tables, the scalar unit otherwise), so rule operands arrive
+// in SGPRs; the per-rule work is a few VALU xor / and-or against them, with an early exit as soon
+// as every lane of the wave has its first match (ballot).  Large tables go through a tuple-space
+// index instead.
 //
-// One launch per batch, persistent workgroups: the grid is what the chip holds at once and
-// workgroup b takes 256-packet tiles b, b + grid, ...  A workgroup keeps its tiles' counters,
-// rule_stats histogram (LDS) and L1 bookkeeping on chip and flushes them once, with device
-// atomics, into replicated per-batch accumulators (replica = workgroup % 32), then takes an
-// arrival ticket.  The workgroup that arrives last folds the accumulators into the worker
-// totals, updates the L1 state and re-arms everything for the next batch.
+// One launch per batch, one persistent 1024-thread workgroup per CU (the grid is what a
+// residency census finds the chip holds at once).  Workgroup b owns 1024-packet tiles b,
+// b + grid, ...; its 16 waves claim the tiles' 64-packet chunks from an LDS counter, so they
+// finish together.  Counters, the rule_stats histogram and the L1 bookkeeping accumulate in LDS
+// (ballots per chunk) and leave once per workgroup, as one device-atomic instruction per kind,
+// into replicated per-batch accumulators.  Nothing waits for anything at the end of a launch:
+// the next launch folds this batch's accumulators (lazy fold), the host reads them after a
+// synchronisation (upe_l1_sync folds the last one).
 //
 // Neighbour lookups answer arp_get_mac / ndp_get_mac exactly without walking the reference's
 // linear-probe chains: at upload the host keeps only the entries a reference probe can reach
 // (probe from the home slot, first valid match before the first invalid slot) and places them
 // by two-choice cuckoo hashing; every answer equals the reference's for the snapshot and a
-// lookup is one round trip (both candidate slots loaded at once).
+// lookup is one LDS read (indexes of up to 2048 slots are staged) or one memory round trip.
 //
 // The worker's one-entry L1 neighbour caches are sequential state (src/worker.c:186-195,
 // 218-225), emulated exactly.  If the starting L1 entry agrees with the
@@ -44,9 +48,8 @@
 // is the final L1 entry: the last table hit, if any packet missed the starting entry and hit the
 // table.  If it disagrees (after a table change, or the calloc'd NDP entry for ::), a packet
 // whose destination equals the starting entry takes the entry's MAC iff no earlier packet missed
-// the entry and hit the table: a workgroup holding such packets flags their tiles and releases
-// its stores, and the last workgroup, which knows the batch's first miss-then-hit index,
-// rewrites them.
+// the entry and hit the table: each 64-packet chunk publishes whether it holds such a packet,
+// and a chunk with candidates looks back over the chunks before it (decoupled look-back).
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -106,8 +109,8 @@ constexpr int kReps = 32;              // replicas of the per-batch accumulators
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
-// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 128 no arrival
-// ticket and no last-workgroup repair, 256 no fold of the previous batch into the L1 state
+// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 256 no fold of the
+// previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
@@ -2061,9 +2064,9 @@ namespace {
 // Credit the sorted-index totals of the current table to rule_stats[rule_id] (device) and clear
 // them: called before the table changes, so a reload keeps every count (src/main.c:216-282
 // swaps rule_stats with the table; here the counts simply carry over by rule_id).
-// Every table size keeps its counts per sorted index, in kStatReps replicas: small tables (the
-// last workgroup adds the folded accumulators to replica 0), mid-size ones (each workgroup's LDS
-// bins) and large ones (upe_rule_hist).  The host sums the replicas and credits rule_id.
+// Every table size keeps its counts per sorted index: small tables in the per-batch replicated
+// accumulators (acc_stats, added here), mid-size ones in kStatReps replicas (each workgroup's LDS
+// bins) and large ones too (upe_rule_hist).  The host sums the replicas and credits rule_id.
 int read_stats_idx(upe_gpu_ctx* c, std::vector<unsigned long long>& idx) {
     const size_t E = 2 * (size_t)c->nrules_pad;
     std::vector<unsigned long long> all(E * kStatReps);
