@@ -75,12 +75,6 @@ namespace {
 constexpr int kBlock = UPE_BLOCK;      // threads per workgroup = packets per tile
 constexpr int kWaves = kBlock / 64;    // 64-packet chunks per tile
 constexpr int kTile = kBlock;
-// Output stores (verdicts, records): plain (0), nontemporal (1), nontemporal in each
-// workgroup's last chunks (2).
-#ifndef UPE_NT_OUT
-#define UPE_NT_OUT 0
-#endif
-constexpr int kNtOut = UPE_NT_OUT;
 
 #ifndef UPE_WAVES_PER_SIMD
 #define UPE_WAVES_PER_SIMD 4
@@ -979,7 +973,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (tid == 0) s_claim = kWaves;
     if (tid < C_N + 3) s_tot[tid] = tid < C_N ? 0u : kNone;
     if (tid < 2 * kWaves) s_wm[tid / 2][tid % 2] = 0u;
-    uint32_t kc = (uint32_t)wave, ch = chunk_of(kc);   // workgroup-local index, chunk
+    uint32_t ch = chunk_of((uint32_t)wave);   // this wave's chunk
     // The first descriptor (its round trip runs under the table staging below), then small
     // rule tables into LDS, before the entry barrier.  (Issuing the first chunk's window loads
     // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
@@ -1063,17 +1057,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // device-scope counters shared by many workgroups cost 2.5 us per 1M batch: every claim
     // serialised on a few hot lines; the LDS counter is private to the workgroup.)
     // Descriptors run one chunk ahead of the frames they point at.
-    uint32_t kcn = 0, chn = kNone;   // this wave's next chunk
-    for (bool first = true; ch != kNone; first = false, ch = chn, kc = kcn) {
+    uint32_t chn = kNone;   // this wave's next chunk
+    for (bool first = true; ch != kNone; first = false, ch = chn) {
         {
             uint32_t kn = 0;
             if (lane == 0) kn = atomicAdd(&s_claim, 1u);
-            kcn = __builtin_amdgcn_readfirstlane(kn);
-            chn = chunk_of(kcn);
+            chn = chunk_of(__builtin_amdgcn_readfirstlane(kn));
         }
-        // nontemporal output stores: everywhere (1), or in the workgroup's last two rounds of
-        // chunks (2), whose lines would otherwise still be dirty in L2 when the launch ends
-        const bool nt = kNtOut == 1 || (kNtOut == 2 && chunk_of(kc + 2u * kWaves) == kNone);
         const uint32_t i = ch * 64u + (uint32_t)lane;
         const bool live = i < a.n;
         const uint64_t dsc = dsc_next;
@@ -1280,13 +1270,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
                              : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
             }
-            if (nt) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 v = {rec.x, rec.y, rec.z, rec.w};
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(&a.hdr[i]));
-            } else {
-                a.hdr[i] = rec;
-            }
+            a.hdr[i] = rec;
         } else if (live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
@@ -1294,10 +1278,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                           (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
-        if (live) {
-            if (nt) __builtin_nontemporal_store(code | flags | rbits, &a.verdict[i]);
-            else a.verdict[i] = code | flags | rbits;
-        }
+        if (live) a.verdict[i] = code | flags | rbits;
         if (a.lens16 && live) a.lens16[i] = (uint16_t)len;   // 2 B/packet for upe_rule_hist
         if (a.flow_hash && live) {
             // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
