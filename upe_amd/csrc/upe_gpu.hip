@@ -1404,84 +1404,124 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // ------------------------------------------------------------------------------------------
 // rule_stats of large tables (more rules than an LDS histogram holds): a group-by of the
 // batch's verdict words by matched rule.  Workgroup (x, y) counts the packets of chunk x whose
-// rule falls in range y in LDS, then adds its nonzero bins to the per-sorted-index totals with
-// contiguous device atomics (credited to rule_id on the host, like small tables).  The device
-// atomics dominate when a chunk sees each rule about once (config D: 64k rules), so chunks are
-// as large as about kHistTarget workgroups allow (fewer, longer workgroups measured slower),
-// and a bin packs packets << 40 | bytes, which cannot overflow: a chunk holds at most 2^24
-// packets of at most 65535 bytes.
+// rule falls in range y in LDS bins (packets << 40 | bytes, which cannot overflow: a chunk holds
+// at most 2^24 packets of at most 65535 bytes), then writes the bins densely into per-chunk
+// partials that upe_hist_reduce sums (or, with UPE_HIST_DENSE=0, adds the nonzero bins with
+// device atomics).  Every range re-reads its chunk (verdict word + the 2-byte length the classify
+// pass left), so ranges are as wide as LDS allows; 1024-thread workgroups with eight packets per
+// thread per round keep enough loads in flight (config D: 256-thread workgroups with four packets
+// a round spent ~300 us per 16M batch waiting on them).
 // ------------------------------------------------------------------------------------------
 #ifndef UPE_HIST_RANGE
-#define UPE_HIST_RANGE 8192
+#define UPE_HIST_RANGE 16384
 #endif
-constexpr uint32_t kHistRange = UPE_HIST_RANGE;   // most rules per workgroup: 64 KB of LDS
+constexpr uint32_t kHistRange = UPE_HIST_RANGE;   // most rules per workgroup: 128 KB of LDS
 constexpr uint32_t kHistChunk = 1u << 24;   // most packets per workgroup
-constexpr uint32_t kHistChunkMin = 4096;
+constexpr uint32_t kHistChunkMin = 8192;
 #ifndef UPE_HIST_TARGET
-#define UPE_HIST_TARGET 2048
+#define UPE_HIST_TARGET 1024
 #endif
 constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
+constexpr int kHistBlock = 1024;
+#ifndef UPE_HIST_DENSE
+#define UPE_HIST_DENSE 1
+#endif
+constexpr bool kHistDense = UPE_HIST_DENSE;   // dense partials + upe_hist_reduce, not atomics
 
-__global__ void __launch_bounds__(256) upe_rule_hist(const uint32_t* verdict, const uint16_t* lens,
-                                                     uint32_t n, uint32_t nrules,
-                                                     unsigned long long* stats_idx,
-                                                     unsigned long long* stats_pk,
-                                                     uint32_t chunk, uint32_t range) {
-    // one 64-bit bin per rule: packets << 40 | bytes
-    extern __shared__ unsigned long long h[];   // [range]
+__global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verdict,
+                                                            const uint16_t* lens, uint32_t n,
+                                                            uint32_t nrules,
+                                                            unsigned long long* stats_idx,
+                                                            unsigned long long* stats_pk,
+                                                            unsigned long long* part,
+                                                            uint32_t chunk, uint32_t range) {
+    extern __shared__ unsigned long long h[];   // [range]: packets << 40 | bytes
     const uint32_t r0 = blockIdx.y * range;
     const uint32_t p0 = blockIdx.x * chunk;
-    for (uint32_t k = threadIdx.x; k < range; k += 256) h[k] = 0;
+    for (uint32_t k = threadIdx.x; k < range; k += kHistBlock) h[k] = 0;
     __syncthreads();
     const uint32_t pend = n - p0 < chunk ? n : p0 + chunk;
-    // four verdict words per thread per round, loaded together
-    for (uint32_t i = p0 + 4 * threadIdx.x; i < pend; i += 4 * 256) {
-        uint32_t v[4];
-        if (i + 4 <= pend && (i & 3) == 0) {
-            const uint4 q = *reinterpret_cast<const uint4*>(verdict + i);
-            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    // eight packets per thread per round: two 16-byte verdict loads and one 16-byte length load
+    // (chunks start at multiples of 8192, so full groups are 16-byte aligned)
+    for (uint32_t i = p0 + 8 * threadIdx.x; i < pend; i += 8 * kHistBlock) {
+        uint32_t v[8], len[8];
+        if (i + 8 <= pend) {
+            const uint4 a0 = *reinterpret_cast<const uint4*>(verdict + i);
+            const uint4 a1 = *reinterpret_cast<const uint4*>(verdict + i + 4);
+            const uint4 l = *reinterpret_cast<const uint4*>(lens + i);
+            v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
+            v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+            len[0] = l.x & 0xFFFFu; len[1] = l.x >> 16; len[2] = l.y & 0xFFFFu; len[3] = l.y >> 16;
+            len[4] = l.z & 0xFFFFu; len[5] = l.z >> 16; len[6] = l.w & 0xFFFFu; len[7] = l.w >> 16;
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = i + j < pend ? verdict[i + j] : 0u;
+            for (int j = 0; j < 8; ++j) {
+                v[j] = i + j < pend ? verdict[i + j] : 0u;
+                len[j] = i + j < pend ? (uint32_t)lens[i + j] : 0u;
+            }
         }
-        // the frame lengths the classify pass left, four to an 8-byte load (a quarter of the
-        // descriptor bytes: every range's workgroups read them again)
-        uint32_t len[4];
-        bool in[4];
-        bool any = false;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 8; ++j) {
             const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
-            in[j] = rb != 0 && rb - 1u - r0 < range;
-            any |= in[j];
+            if (rb != 0 && rb - 1u - r0 < range) atomicAdd(&h[rb - 1u - r0], (1ull << 40) | len[j]);
         }
-        if (any && i + 4 <= pend && (i & 3) == 0) {
-            const uint2 q = *reinterpret_cast<const uint2*>(lens + i);
-            len[0] = q.x & 0xFFFFu; len[1] = q.x >> 16; len[2] = q.y & 0xFFFFu; len[3] = q.y >> 16;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) len[j] = in[j] ? (uint32_t)lens[i + j] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (in[j]) atomicAdd(&h[(v[j] >> 8) - 1u - r0], (1ull << 40) | len[j]);
     }
     __syncthreads();
     const uint32_t rend = nrules - r0 < range ? nrules : r0 + range;
+    if (part) {
+        // dense: this chunk's bins, zeros included, as plain coalesced stores (upe_hist_reduce
+        // sums them over the chunks; no device atomics)
+        unsigned long long* o = part + (size_t)blockIdx.x * nrules + r0;
+        for (uint32_t k = threadIdx.x; k < rend - r0; k += kHistBlock) o[k] = h[k];
+        return;
+    }
     if (stats_pk) {
         // one packed atomic per bin (the launch checked that a replica's packets fit 24 bits, so
         // its bytes fit 40); upe_stats_unpack adds the packed words to stats_idx afterwards
         unsigned long long* pk = stats_pk + (size_t)(blockIdx.x % kStatReps) * nrules + r0;
-        for (uint32_t k = threadIdx.x; k < rend - r0; k += 256) {
+        for (uint32_t k = threadIdx.x; k < rend - r0; k += kHistBlock) {
             const unsigned long long b = h[k];
             if (b) atomicAdd(&pk[k], b);
         }
         return;
     }
-    for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += 256) {
+    for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += kHistBlock) {
         const unsigned long long b = h[k >> 1];
         const unsigned long long x = (k & 1) ? (b & ((1ull << 40) - 1)) : (b >> 40);
         if (x) atomicAdd(&stats_idx[(size_t)(blockIdx.x % kStatReps) * 2 * nrules + 2 * (size_t)r0 + k], x);
+    }
+}
+
+// The dense group-by partials ([nchunks][nrules], packets << 40 | bytes) summed over the chunks:
+// slice y of the grid sums chunks y, y + S, ... for rule r = blockIdx.x * 256 + thread and adds
+// the unpacked totals to replica y % kStatReps of stats_idx; with S = kStatReps every replica
+// word has exactly one writer in the launch, so the adds are plain.
+__global__ void __launch_bounds__(256) upe_hist_reduce(const unsigned long long* part,
+                                                       uint32_t nchunks, uint32_t nrules,
+                                                       unsigned long long* stats_idx) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrules) return;
+    unsigned long long pk = 0, by = 0;
+    uint32_t c = blockIdx.y;
+    for (; c + 7 * gridDim.y < nchunks; c += 8 * gridDim.y) {
+        unsigned long long b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = part[(size_t)(c + j * gridDim.y) * nrules + r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            pk += b[j] >> 40;
+            by += b[j] & ((1ull << 40) - 1);
+        }
+    }
+    for (; c < nchunks; c += gridDim.y) {
+        const unsigned long long b = part[(size_t)c * nrules + r];
+        pk += b >> 40;
+        by += b & ((1ull << 40) - 1);
+    }
+    if (pk) {
+        unsigned long long* o = stats_idx + (size_t)(blockIdx.y % kStatReps) * 2 * nrules + 2 * (size_t)r;
+        o[0] += pk;
+        o[1] += by;
     }
 }
 
@@ -1634,6 +1674,8 @@ struct upe_gpu_ctx {
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
     unsigned long long* stats_pk = nullptr;    // [kStatReps][rules_alloc] one batch, packed
+    unsigned long long* hist_part = nullptr;   // [chunks][nrules_pad] dense group-by partials
+    size_t hist_part_alloc = 0;
     uint16_t* lens16 = nullptr;                // [lens_alloc] frame lengths (group-by tables)
     size_t lens_alloc = 0;
     std::vector<int2> rinfo_host;              // (action, rule_id) per sorted index
@@ -2024,7 +2066,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->stats_pk, c->lens16, c->arp, c->ndp, c->st, c->stats,
                     c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
-                    c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens};
+                    c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
+                    c->hist_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -2581,11 +2624,33 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         // packed bins when no replica can collect 2^24 packets (nor so 2^40 bytes) in one batch
         const uint64_t per_rep = (uint64_t)((hg.x + kStatReps - 1) / kStatReps) * chunk;
         const bool packed = per_rep < (1ull << 24);
-        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(256), range * sizeof(unsigned long long), s,
+        // dense partials (one 8-byte bin per chunk and rule, summed by upe_hist_reduce) instead
+        // of device atomics per nonzero bin
+        const size_t part_words = (size_t)hg.x * c->nrules_pad;
+        const bool dense = kHistDense;
+        if (dense && part_words > c->hist_part_alloc) {
+            if (c->hist_part) (void)hipFree(c->hist_part);
+            c->hist_part = nullptr;
+            c->hist_part_alloc = 0;
+            HIP_TRY(hipMalloc(&c->hist_part, part_words * sizeof(unsigned long long)));
+            c->hist_part_alloc = part_words;
+        }
+        static std::atomic<uint64_t> hist_attr{0};   // 128 KB of dynamic LDS, once per device
+        if (!(hist_attr.fetch_or(1ull << (c->device & 63)) & (1ull << (c->device & 63))))
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_rule_hist),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(kHistRange * sizeof(unsigned long long)));
+        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(kHistBlock), range * sizeof(unsigned long long), s,
                            d_verdict, c->lens16, (uint32_t)n, c->nrules_pad, c->stats_idx,
-                           packed ? c->stats_pk : nullptr, chunk, range);
+                           packed && !dense ? c->stats_pk : nullptr,
+                           dense ? c->hist_part : nullptr, chunk,
+                           range);
         HIP_TRY(hipGetLastError());
-        if (packed) {
+        if (dense) {
+            hipLaunchKernelGGL(upe_hist_reduce, dim3((c->nrules_pad + 255) / 256, kStatReps),
+                               dim3(256), 0, s, c->hist_part, hg.x, c->nrules_pad, c->stats_idx);
+            HIP_TRY(hipGetLastError());
+        } else if (packed) {
             const uint32_t words = kStatReps * c->nrules_pad;
             hipLaunchKernelGGL(upe_stats_unpack, dim3((words + 255) / 256), dim3(256), 0, s,
                                c->stats_pk, c->stats_idx, words);
