@@ -87,6 +87,11 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
+// Tuple-space probes of both families in one loop (1) or one family after the other (0).
+#ifndef UPE_TSS_BOTH
+#define UPE_TSS_BOTH 1
+#endif
+constexpr bool kTssBoth = UPE_TSS_BOTH;
 // Neighbour indexes staged in LDS (one workgroup per CU, so a CU reads them once per launch):
 // ARP up to 2048 slots (32 KB), NDP up to 2048 slots (64 KB), within kLdsDynMax of dynamic LDS.
 #ifndef UPE_ARP_LDS_SLOTS
@@ -669,6 +674,98 @@ __device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32
     return best;
 }
 
+// Both families in one probe loop: each lane takes its own family's group descriptor,
+// fingerprint array and slot table, so a wave that mixes IPv4 and IPv6 packets waits for one
+// fingerprint and one slot round trip per group index instead of one per family.  At most one
+// slot per lane and group is read — the first whose fingerprint matches; a lane whose two
+// fingerprints both match and whose first slot holds another key reads the second one in a
+// (rare) extra step.  Same answer as tss_match<4> / tss_match<6>, group by group.
+__device__ __forceinline__ uint32_t tss_fmix(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, bool is6,
+                                                   uint32_t k0, uint32_t k1, const uint32_t s[4],
+                                                   const uint32_t d[4], uint32_t& act) {
+    uint32_t best = kNone;
+    const uint32_t ng = a.ng4 > a.ng6 ? a.ng4 : a.ng6;
+    const uint32_t ngf = is6 ? a.ng6 : a.ng4;
+    const auto* G4 = as_const<u32x16>(a.tg4);
+    const auto* G6 = as_const<u32x16>(a.tg6);
+    const uint16_t* FP = is6 ? a.tf6 : a.tf4;
+    const uint4* T = is6 ? a.tt6 : a.tt4;
+    const uint32_t st = is6 ? 3u : 2u;   // slot stride in uint4
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t gu = __builtin_amdgcn_readfirstlane(g);
+        u32x16 q4 = {}, q6 = {};
+        if (gu < a.ng4) q4 = G4[gu];
+        if (gu < a.ng6) q6 = G6[gu];
+        // groups ascend by smallest sorted index within each family: once no lane wants group
+        // g, no lane wants a later one
+        const bool want = active && g < ngf && best > (is6 ? q6[10] : q4[10]);
+        if (!__any(want)) break;
+        if (want) {
+            uint32_t q[14];
+#pragma unroll
+            for (int j = 0; j < 14; ++j) q[j] = is6 ? q6[j] : q4[j];
+            uint32_t kw[10];
+            kw[0] = k0 & q[0];
+            kw[1] = k1 & q[1];
+            kw[2] = s[0] & q[2];
+            kw[3] = is6 ? (s[1] & q[4]) : (d[0] & q[3]);
+            kw[4] = s[2] & q[5]; kw[5] = s[3] & q[6]; kw[6] = d[0] & q[3];
+            kw[7] = d[1] & q[7]; kw[8] = d[2] & q[8]; kw[9] = d[3] & q[9];
+            // tss_hash over 4 words (IPv4) or 10 (IPv6), bit for bit
+            uint32_t h = q[12] ^ 0x9E3779B9u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                h = (h ^ kw[j]) * 0x01000193u;
+                h ^= h >> 15;
+            }
+            uint32_t h6 = h;
+#pragma unroll
+            for (int j = 4; j < 10; ++j) {
+                h6 = (h6 ^ kw[j]) * 0x01000193u;
+                h6 ^= h6 >> 15;
+            }
+            h = tss_fmix(is6 ? h6 : h);
+            const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
+            const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
+            const uint32_t tag = tss_tag(h);
+            const bool m1 = FP[t1] == tag, m2 = FP[t2] == tag;
+            uint32_t idx = kNone, ac = 0;
+            auto probe = [&](uint32_t t) {
+                const uint4 A = T[st * t], B = T[st * t + 1];
+                uint4 C = make_uint4(0, 0, 0, 0);
+                if (is6) C = T[st * t + 2];
+                const bool k4 = A.x == kw[0] && A.y == kw[1] && A.z == kw[2] && A.w == kw[3];
+                const bool hit = is6 ? ((C.w & 1u) && k4 && B.x == kw[4] && B.y == kw[5] &&
+                                        B.z == kw[6] && B.w == kw[7] && C.x == kw[8] &&
+                                        C.y == kw[9])
+                                     : (B.y != 0u && k4);
+                if (hit) {
+                    idx = is6 ? C.z : B.x;
+                    ac = is6 ? (C.w >> 8) : B.z;
+                }
+                return hit;
+            };
+            if (m1 || m2) {
+                const bool hit = probe(m1 ? t1 : t2);
+                if (!hit && m1 && m2) probe(t2);
+            }
+            if (idx < best) {
+                best = idx;
+                act = ac << 16;
+            }
+        }
+    }
+    return best;
+}
+
 // ------------------------------------------------------------------------------------------
 // General path: every live packet the fast path does not cover (ARP and NDP control frames,
 // IPv4 with options, truncated, foreign or malformed frames).  Same outputs as the fast path.
@@ -1159,6 +1256,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (kAblate & 1) {
             ri = ok ? 0u : kNone;
             act = 1u << 16;
+        } else if (kTssMode && kTssBoth) {
+            ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act);
         } else if (kTssMode) {
             uint32_t a4 = 0, a6 = 0;
             const uint32_t r4 = tss_match<4>(a, ok && !r.v6, k0, k1, r.s, r.d, a4);
