@@ -216,6 +216,8 @@ struct NeighIndex {
 //   [0] m0 (proto, src_port masks)  [1] m1 (dst_port mask)  [2] src word-0 mask
 //   [3] dst word-0 mask  [4..6] src words 1-3 masks  [7..9] dst words 1-3 masks (family 6)
 //   [10] smallest sorted index in the group  [11] log2(slots)  [12] seed  [13] first slot
+//   [14] 1 | action << 8 when every mask word is zero (a catch-all group: every packet of the
+//        family matches its one key, so the probe needs no memory access), else 0
 // Slots: family 4 = 2 x uint4 {k0, k1, s0, d0}, {index, used, -, -};
 //        family 6 = 3 x uint4 {k0, k1, s0, s1}, {s2, s3, d0, d1}, {d2, d3, index, used}.
 struct __attribute__((aligned(16))) TssGroup {
@@ -708,7 +710,14 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
         // g, no lane wants a later one
         const bool want = active && g < ngf && best > (is6 ? q6[10] : q4[10]);
         if (!__any(want)) break;
-        if (want) {
+        const uint32_t cw = is6 ? q6[14] : q4[14];
+        if (want && (cw & 1u)) {
+            // catch-all group: the key matches (every mask is zero), its index is the group's
+            if ((is6 ? q6[10] : q4[10]) < best) {
+                best = is6 ? q6[10] : q4[10];
+                act = (cw >> 8) << 16;
+            }
+        } else if (want) {
             uint32_t q[14];
 #pragma unroll
             for (int j = 0; j < 14; ++j) q[j] = is6 ? q6[j] : q4[j];
@@ -2309,6 +2318,10 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
         d.w[11] = bits;
         d.w[12] = seed;
         d.w[13] = (uint32_t)(out.slots.size() / per);
+        bool wild = true;
+        for (int j = 0; j < 10; ++j) wild = wild && sg[j] == 0;
+        if (wild && idx.size() == 1)
+            d.w[14] = 1u | (act_code(rules[idx[0]].action.type) << 8);
         out.groups.push_back(d);
         const size_t base = out.slots.size();
         out.slots.resize(base + slot.size() * per, make_uint4(0, 0, 0, 0));
