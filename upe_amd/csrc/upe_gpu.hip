@@ -787,29 +787,31 @@ struct Parsed {
     uint32_t ttl, c1w1, c1w2;      // TTL / hop, and bytes 20..27 as they are forwarded
 };
 
-// Inlined (only waves holding such a packet run it).  An out-of-line call (UPE_GP_CALL=1, a
-// diagnostic build) saves the caller's live registers to scratch, ~100 bytes of private-memory
-// traffic per slow packet (config D: 1.7 GB written per 16M batch), and a kernel with a scratch
-// stack depends on the runtime's scratch allocation for its residency; inlined, every classify
-// kernel but one runs without scratch at the 128-VGPR budget.
+// Inlined (only waves holding such a packet run it).  An out-of-line call (measured in round 2)
+// saved the caller's live registers to scratch, ~100 bytes of private-memory traffic per slow
+// packet (config D: 1.7 GB written per 16M batch); inlined, the classify kernels run without
+// scratch at the 128-VGPR budget.  The path reuses the fast path's window (bytes 0..79, chunks
+// at or past len zero) and loads bytes 80..95 only for frames that have them: it reads no byte
+// at or past len except the ARP header, which masks them (len_mask), and its ARP reply stores
+// bytes 0..47, which the window always holds as loaded.
 struct Port {
     uint32_t mac_lo, mac_hi, ip4;
 };
-__device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r) {
+__device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r,
+                                             const uint32_t (&win)[20]) {
     r.ok = false; r.consumed = false; r.v6 = false; r.flags = 0;
     r.proto = r.sport = r.dport = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) r.s[j] = r.d[j] = 0;
     r.ttl = 0;
-    // its own copy of the window (the frame is in cache): bytes 0..95, IPv4 options reach 94
+    // bytes 0..95 (IPv4 options reach 94): the window, and bytes 80..95 when the frame has them
     uint32_t w[24];
-    {
-        const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            const uint4 v = q[c];
-            w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-        }
+    for (int j = 0; j < 20; ++j) w[j] = win[j];
+    w[20] = w[21] = w[22] = w[23] = 0;
+    if (len > 80u) {
+        const uint4 v = reinterpret_cast<const uint4*>(p)[5];
+        w[20] = v.x; w[21] = v.y; w[22] = v.z; w[23] = v.w;
     }
     r.c1w1 = w[5];
     r.c1w2 = w[6];
@@ -926,14 +928,6 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
         }
     }
 }
-#ifndef UPE_GP_CALL
-#define UPE_GP_CALL 0   // 1: the scan kernel calls the general path out of line (scratch stack)
-#endif
-#if UPE_GP_CALL
-__device__ __noinline__ void general_path_call(Port a, uint8_t* p, uint32_t len, Parsed& r) {
-    general_path(a, p, len, r);
-}
-#endif
 
 // ------------------------------------------------------------------------------------------
 // Decoupled look-back (only while a starting L1 entry disagrees with the table).  A packet whose
@@ -1232,12 +1226,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const bool slow = live && !fast4 && !fast6;
         if (__any(slow) && slow) {
             Parsed g;
-#if UPE_GP_CALL
-            if constexpr (!kTssMode)
-                general_path_call(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
-            else
-#endif
-                general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g);
+            general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g, w);
             r = g;
         }
 
