@@ -87,11 +87,6 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
-// Tuple-space probes of both families in one loop (1) or one family after the other (0).
-#ifndef UPE_TSS_BOTH
-#define UPE_TSS_BOTH 1
-#endif
-constexpr bool kTssBoth = UPE_TSS_BOTH;
 // Neighbour indexes staged in LDS (one workgroup per CU, so a CU reads them once per launch):
 // ARP up to 2048 slots (32 KB), NDP up to 2048 slots (64 KB), within kLdsDynMax of dynamic LDS.
 #ifndef UPE_ARP_LDS_SLOTS
@@ -603,85 +598,16 @@ __host__ __device__ __forceinline__ uint16_t tss_tag(uint32_t h) {
     return (uint16_t)((h & 0xFFFFu) | 1u);
 }
 
-// First match through the tuple-space index for one packet family (F = 4 or 6).  Groups are
-// visited in order of their smallest sorted index, so once a lane's best index is below the
-// next group's smallest, nothing later can precede it: the result is exactly the first match
-// of the linear scan (reference src/rule_table.c:163-176).
-template <int F>
-__device__ __forceinline__ uint32_t tss_match(const Args& a, bool active, uint32_t k0, uint32_t k1,
-                                              const uint32_t s[4], const uint32_t d[4],
-                                              uint32_t& act) {
-    uint32_t best = kNone;
-    const uint32_t ng = F == 4 ? a.ng4 : a.ng6;
-    const auto* G = as_const<u32x16>(F == 4 ? a.tg4 : a.tg6);
-    const uint4* T = F == 4 ? a.tt4 : a.tt6;
-    for (uint32_t g = 0; g < ng; ++g) {
-        const u32x16 q = G[__builtin_amdgcn_readfirstlane(g)];
-        const bool want = active && best > q[10];
-        if (!__any(want)) break;
-        if (want) {
-            constexpr int nw = F == 4 ? 4 : 10;
-            uint32_t kw[nw];
-            kw[0] = k0 & q[0];
-            kw[1] = k1 & q[1];
-            kw[2] = s[0] & q[2];
-            if constexpr (F == 4) {
-                kw[3] = d[0] & q[3];
-            } else {
-                kw[3] = s[1] & q[4]; kw[4] = s[2] & q[5]; kw[5] = s[3] & q[6];
-                kw[6] = d[0] & q[3];
-                kw[7] = d[1] & q[7]; kw[8] = d[2] & q[8]; kw[9] = d[3] & q[9];
-            }
-            const uint32_t h = tss_hash(kw, nw, q[12]);
-            const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
-            const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
-            // fingerprints first (a few hundred KB, L2-resident): a slot is loaded only when
-            // its fingerprint matches, and then compared in full
-            const uint16_t* FP = F == 4 ? a.tf4 : a.tf6;
-            const uint32_t tag = tss_tag(h);
-            const bool m1 = FP[t1] == tag, m2 = FP[t2] == tag;
-            uint32_t idx = kNone;
-            if (m1 || m2) {
-                if constexpr (F == 4) {
-                    uint4 a1 = make_uint4(0, 0, 0, 0), b1 = a1, a2 = a1, b2 = a1;
-                    if (m1) { a1 = T[2 * t1]; b1 = T[2 * t1 + 1]; }
-                    if (m2) { a2 = T[2 * t2]; b2 = T[2 * t2 + 1]; }
-                    const bool h1 = m1 && b1.y && a1.x == kw[0] && a1.y == kw[1] &&
-                                    a1.z == kw[2] && a1.w == kw[3];
-                    const bool h2 = m2 && b2.y && a2.x == kw[0] && a2.y == kw[1] &&
-                                    a2.z == kw[2] && a2.w == kw[3];
-                    idx = h1 ? b1.x : h2 ? b2.x : kNone;
-                    const uint32_t ac = h1 ? b1.z : b2.z;
-                    if (idx < best) act = ac << 16;
-                } else {
-                    uint4 a1 = make_uint4(0, 0, 0, 0), b1 = a1, c1 = a1, a2 = a1, b2 = a1, c2 = a1;
-                    if (m1) { a1 = T[3 * t1]; b1 = T[3 * t1 + 1]; c1 = T[3 * t1 + 2]; }
-                    if (m2) { a2 = T[3 * t2]; b2 = T[3 * t2 + 1]; c2 = T[3 * t2 + 2]; }
-                    const bool h1 = m1 && (c1.w & 1u) && a1.x == kw[0] && a1.y == kw[1] &&
-                                    a1.z == kw[2] && a1.w == kw[3] && b1.x == kw[4] &&
-                                    b1.y == kw[5] && b1.z == kw[6] && b1.w == kw[7] &&
-                                    c1.x == kw[8] && c1.y == kw[9];
-                    const bool h2 = m2 && (c2.w & 1u) && a2.x == kw[0] && a2.y == kw[1] &&
-                                    a2.z == kw[2] && a2.w == kw[3] && b2.x == kw[4] &&
-                                    b2.y == kw[5] && b2.z == kw[6] && b2.w == kw[7] &&
-                                    c2.x == kw[8] && c2.y == kw[9];
-                    idx = h1 ? c1.z : h2 ? c2.z : kNone;
-                    const uint32_t ac = (h1 ? c1.w : c2.w) >> 8;
-                    if (idx < best) act = ac << 16;
-                }
-            }
-            best = min(best, idx);
-        }
-    }
-    return best;
-}
-
-// Both families in one probe loop: each lane takes its own family's group descriptor,
-// fingerprint array and slot table, so a wave that mixes IPv4 and IPv6 packets waits for one
-// fingerprint and one slot round trip per group index instead of one per family.  At most one
+// First match through the tuple-space index.  Groups are visited in order of their smallest
+// sorted index, so once a lane's best index is below the next group's smallest, nothing later
+// can precede it: the result is exactly the first match of the linear scan (reference
+// src/rule_table.c:163-176).  Both families share one probe loop: each lane takes its own
+// family's group descriptor, fingerprint array and slot table, so a wave that mixes IPv4 and
+// IPv6 packets waits for one fingerprint and one slot round trip per group index, not one per
+// family (one loop per family measured 1024 vs 940 us per config-D batch).  At most one
 // slot per lane and group is read — the first whose fingerprint matches; a lane whose two
 // fingerprints both match and whose first slot holds another key reads the second one in a
-// (rare) extra step.  Same answer as tss_match<4> / tss_match<6>, group by group.
+// (rare) extra step.
 __device__ __forceinline__ uint32_t tss_fmix(uint32_t h) {
     h ^= h >> 16;
     h *= 0x85EBCA6Bu;
@@ -1254,15 +1180,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (kAblate & 1) {
             ri = ok ? 0u : kNone;
             act = 1u << 16;
-        } else if (kTssMode && kTssBoth) {
-            ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act);
         } else if (kTssMode) {
-            uint32_t a4 = 0, a6 = 0;
-            const uint32_t r4 = tss_match<4>(a, ok && !r.v6, k0, k1, r.s, r.d, a4);
-            const uint32_t r6 =
-                need_v6 ? tss_match<6>(a, ok && r.v6, k0, k1, r.s, r.d, a6) : kNone;
-            ri = r.v6 ? r6 : r4;
-            act = r.v6 ? a6 : a4;
+            ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act);
         } else {
             if (small_stats)
                 ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
@@ -1503,8 +1422,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // batch's verdict words by matched rule.  Workgroup (x, y) counts the packets of chunk x whose
 // rule falls in range y in LDS bins (packets << 40 | bytes, which cannot overflow: a chunk holds
 // at most 2^24 packets of at most 65535 bytes), then writes the bins densely into per-chunk
-// partials that upe_hist_reduce sums (or, with UPE_HIST_DENSE=0, adds the nonzero bins with
-// device atomics).  Every range re-reads its chunk (verdict word + the 2-byte length the classify
+// partials that upe_hist_reduce sums (device atomics per nonzero bin, measured in round 2, were
+// no faster and needed a packed staging array).  Every range re-reads its chunk (verdict word + the 2-byte length the classify
 // pass left), so ranges are as wide as LDS allows; 1024-thread workgroups with eight packets per
 // thread per round keep enough loads in flight (config D: 256-thread workgroups with four packets
 // a round spent ~300 us per 16M batch waiting on them).
@@ -1520,16 +1439,10 @@ constexpr uint32_t kHistChunkMin = 8192;
 #endif
 constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
 constexpr int kHistBlock = 1024;
-#ifndef UPE_HIST_DENSE
-#define UPE_HIST_DENSE 1
-#endif
-constexpr bool kHistDense = UPE_HIST_DENSE;   // dense partials + upe_hist_reduce, not atomics
 
 __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verdict,
                                                             const uint16_t* lens, uint32_t n,
                                                             uint32_t nrules,
-                                                            unsigned long long* stats_idx,
-                                                            unsigned long long* stats_pk,
                                                             unsigned long long* part,
                                                             uint32_t chunk, uint32_t range) {
     extern __shared__ unsigned long long h[];   // [range]: packets << 40 | bytes
@@ -1564,29 +1477,11 @@ __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verd
         }
     }
     __syncthreads();
+    // this chunk's bins, zeros included, as plain coalesced stores (upe_hist_reduce sums them
+    // over the chunks; no device atomics)
     const uint32_t rend = nrules - r0 < range ? nrules : r0 + range;
-    if (part) {
-        // dense: this chunk's bins, zeros included, as plain coalesced stores (upe_hist_reduce
-        // sums them over the chunks; no device atomics)
-        unsigned long long* o = part + (size_t)blockIdx.x * nrules + r0;
-        for (uint32_t k = threadIdx.x; k < rend - r0; k += kHistBlock) o[k] = h[k];
-        return;
-    }
-    if (stats_pk) {
-        // one packed atomic per bin (the launch checked that a replica's packets fit 24 bits, so
-        // its bytes fit 40); upe_stats_unpack adds the packed words to stats_idx afterwards
-        unsigned long long* pk = stats_pk + (size_t)(blockIdx.x % kStatReps) * nrules + r0;
-        for (uint32_t k = threadIdx.x; k < rend - r0; k += kHistBlock) {
-            const unsigned long long b = h[k];
-            if (b) atomicAdd(&pk[k], b);
-        }
-        return;
-    }
-    for (uint32_t k = threadIdx.x; k < 2 * (rend - r0); k += kHistBlock) {
-        const unsigned long long b = h[k >> 1];
-        const unsigned long long x = (k & 1) ? (b & ((1ull << 40) - 1)) : (b >> 40);
-        if (x) atomicAdd(&stats_idx[(size_t)(blockIdx.x % kStatReps) * 2 * nrules + 2 * (size_t)r0 + k], x);
-    }
+    unsigned long long* o = part + (size_t)blockIdx.x * nrules + r0;
+    for (uint32_t k = threadIdx.x; k < rend - r0; k += kHistBlock) o[k] = h[k];
 }
 
 // The dense group-by partials ([nchunks][nrules], packets << 40 | bytes) summed over the chunks:
@@ -1619,20 +1514,6 @@ __global__ void __launch_bounds__(256) upe_hist_reduce(const unsigned long long*
         unsigned long long* o = stats_idx + (size_t)(blockIdx.y % kStatReps) * 2 * nrules + 2 * (size_t)r;
         o[0] += pk;
         o[1] += by;
-    }
-}
-
-// The packed group-by totals of one batch into stats_idx ([kStatReps][nrules][2]), re-armed to
-// zero.  Each word has one thread, and nothing else touches either array until the next launch.
-__global__ void __launch_bounds__(256) upe_stats_unpack(unsigned long long* stats_pk,
-                                                        unsigned long long* stats_idx,
-                                                        uint32_t words) {
-    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < words; e += gridDim.x * 256) {
-        const unsigned long long b = stats_pk[e];
-        if (!b) continue;
-        stats_pk[e] = 0;
-        stats_idx[2 * (size_t)e] += b >> 40;
-        stats_idx[2 * (size_t)e + 1] += b & ((1ull << 40) - 1);
     }
 }
 
@@ -1770,7 +1651,6 @@ struct upe_gpu_ctx {
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
-    unsigned long long* stats_pk = nullptr;    // [kStatReps][rules_alloc] one batch, packed
     unsigned long long* hist_part = nullptr;   // [chunks][nrules_pad] dense group-by partials
     size_t hist_part_alloc = 0;
     uint16_t* lens16 = nullptr;                // [lens_alloc] frame lengths (group-by tables)
@@ -2161,7 +2041,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->stats_pk, c->lens16, c->arp, c->ndp, c->st, c->stats,
+    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->lens16, c->arp, c->ndp, c->st, c->stats,
                     c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
                     c->hist_part};
@@ -2416,13 +2296,9 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         HIP_TRY(hipMalloc(&c->rv6, pad * sizeof(RuleV6)));
         HIP_TRY(hipMalloc(&c->rinfo, pad * sizeof(int2)));
         if (c->stats_idx) (void)hipFree(c->stats_idx);
-        if (c->stats_pk) (void)hipFree(c->stats_pk);
         c->stats_idx = nullptr;
-        c->stats_pk = nullptr;
         HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * kStatReps * sizeof(unsigned long long)));
         HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * kStatReps * sizeof(unsigned long long)));
-        HIP_TRY(hipMalloc(&c->stats_pk, pad * kStatReps * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(c->stats_pk, 0, pad * kStatReps * sizeof(unsigned long long)));
         c->rules_alloc = pad;
         if (publish(c) != 0) return -1;
     }
@@ -2722,14 +2598,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         while (chunk > kHistChunkMin && ((n + chunk / 2 - 1) / (chunk / 2)) * nr <= kHistTarget)
             chunk >>= 1;
         const dim3 hg((uint32_t)((n + chunk - 1) / chunk), nr);
-        // packed bins when no replica can collect 2^24 packets (nor so 2^40 bytes) in one batch
-        const uint64_t per_rep = (uint64_t)((hg.x + kStatReps - 1) / kStatReps) * chunk;
-        const bool packed = per_rep < (1ull << 24);
-        // dense partials (one 8-byte bin per chunk and rule, summed by upe_hist_reduce) instead
-        // of device atomics per nonzero bin
+        // dense partials: one 8-byte bin per chunk and rule, summed by upe_hist_reduce
         const size_t part_words = (size_t)hg.x * c->nrules_pad;
-        const bool dense = kHistDense;
-        if (dense && part_words > c->hist_part_alloc) {
+        if (part_words > c->hist_part_alloc) {
             if (c->hist_part) (void)hipFree(c->hist_part);
             c->hist_part = nullptr;
             c->hist_part_alloc = 0;
@@ -2742,21 +2613,12 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)(kHistRange * sizeof(unsigned long long)));
         hipLaunchKernelGGL(upe_rule_hist, hg, dim3(kHistBlock), range * sizeof(unsigned long long), s,
-                           d_verdict, c->lens16, (uint32_t)n, c->nrules_pad, c->stats_idx,
-                           packed && !dense ? c->stats_pk : nullptr,
-                           dense ? c->hist_part : nullptr, chunk,
+                           d_verdict, c->lens16, (uint32_t)n, c->nrules_pad, c->hist_part, chunk,
                            range);
         HIP_TRY(hipGetLastError());
-        if (dense) {
-            hipLaunchKernelGGL(upe_hist_reduce, dim3((c->nrules_pad + 255) / 256, kStatReps),
-                               dim3(256), 0, s, c->hist_part, hg.x, c->nrules_pad, c->stats_idx);
-            HIP_TRY(hipGetLastError());
-        } else if (packed) {
-            const uint32_t words = kStatReps * c->nrules_pad;
-            hipLaunchKernelGGL(upe_stats_unpack, dim3((words + 255) / 256), dim3(256), 0, s,
-                               c->stats_pk, c->stats_idx, words);
-            HIP_TRY(hipGetLastError());
-        }
+        hipLaunchKernelGGL(upe_hist_reduce, dim3((c->nrules_pad + 255) / 256, kStatReps),
+                           dim3(256), 0, s, c->hist_part, hg.x, c->nrules_pad, c->stats_idx);
+        HIP_TRY(hipGetLastError());
     }
     if (c->t_left && --c->t_left == 0) {
         HIP_TRY(hipEventRecord(c->ev[c->ev_used + 1], s));
