@@ -87,6 +87,11 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsStatsMax = UPE_LDS_STATS_MAX;   // rule_stats in the classify kernel's LDS up to here
 constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (summed on the host)
+// Claim the next chunk after finishing the current one once this few chunks are unclaimed.
+#ifndef UPE_LATE_CLAIM
+#define UPE_LATE_CLAIM 16
+#endif
+constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 // Neighbour indexes staged in LDS (one workgroup per CU, so a CU reads them once per launch):
 // ARP up to 2048 slots (32 KB), NDP up to 2048 slots (64 KB), within kLdsDynMax of dynamic LDS.
 #ifndef UPE_ARP_LDS_SLOTS
@@ -1083,12 +1088,31 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // device-scope counters shared by many workgroups cost 2.5 us per 1M batch: every claim
     // serialised on a few hot lines; the LDS counter is private to the workgroup.)
     // Descriptors run one chunk ahead of the frames they point at.
+    // The workgroup's number of chunks: a wave claims its next chunk one ahead (so that its
+    // descriptors arrive while it works) only while more than kLateClaim chunks are unclaimed;
+    // after that it claims when it has finished its chunk, so that near the end no wave holds
+    // an unstarted chunk while another waits with nothing.
+    uint32_t nloc = 0;
+    if (blockIdx.x < a.ntiles) {
+        const uint32_t own = (a.ntiles - 1u - blockIdx.x) / gridDim.x + 1u;
+        const uint32_t tl = blockIdx.x + (own - 1u) * gridDim.x;
+        const uint32_t lc = min((uint32_t)kWaves, (a.n - tl * (uint32_t)kTile + 63u) / 64u);
+        nloc = (own - 1u) * (uint32_t)kWaves + lc;
+    }
+    auto claim = [&]() {
+        uint32_t kn = 0;
+        if (lane == 0) kn = atomicAdd(&s_claim, 1u);
+        return chunk_of(__builtin_amdgcn_readfirstlane(kn));
+    };
     uint32_t chn = kNone;   // this wave's next chunk
     for (bool first = true; ch != kNone; first = false, ch = chn) {
+        bool late;
         {
-            uint32_t kn = 0;
-            if (lane == 0) kn = atomicAdd(&s_claim, 1u);
-            chn = chunk_of(__builtin_amdgcn_readfirstlane(kn));
+            uint32_t cur = 0;
+            if (lane == 0)
+                cur = __hip_atomic_load(&s_claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            late = __builtin_amdgcn_readfirstlane(cur) + kLateClaim >= nloc;
+            chn = late ? kNone : claim();
         }
         const uint32_t i = ch * 64u + (uint32_t)lane;
         const bool live = i < a.n;
@@ -1345,6 +1369,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 s_pay[wave][3] = r.d[0]; s_pay[wave][4] = r.d[1]; s_pay[wave][5] = r.d[2];
                 s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
             }
+        }
+        if (late) {
+            chn = claim();
+            dsc_next = 0;
+            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
         }
     }
     STAMP(4);
