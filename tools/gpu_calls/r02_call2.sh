@@ -1,5 +1,5 @@
-# round 2 profiles of the chunk-claim kernel: default bench line (B, emit, cpu_baseline, host
-# round trip), kernel-trace stats for B / C / D, PMC traffic for B / C / D in emit mode, stamps
+# round 2 profiles: default bench line (B, emit, cpu_baseline, host round trip), kernel-trace
+# stats for B / C / D, PMC traffic for B / C / D in emit mode, stamps
 bash tools/gpu_session.sh \
  "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
  "benchB:400:python bench.py --host-reps 10 > gpurun_out/benchB.json" \
