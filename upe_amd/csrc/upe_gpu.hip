@@ -195,7 +195,7 @@ struct DevState {
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
     uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
-    uint32_t* lb;                    // [ntiles * kWaves] look-back flags
+    uint32_t* lb;                    // look-back flags, one per 64-packet chunk
     unsigned long long* stats;       // [cap][2] worker rule_stats (mid-size and large tables)
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2] totals per sorted index
 };
@@ -230,7 +230,6 @@ struct Args {
     const uint64_t* desc;
     uint32_t* verdict;
     uint32_t n;
-    uint32_t ntiles;
     const RuleV4* rv4;
     const RuleV6* rv6;
     const int2* rinfo;
@@ -260,8 +259,10 @@ struct Args {
     uint32_t k6;
     uint32_t paycap;                 // a.pay[(k % 2) * paycap + workgroup]
     uint32_t census;                 // non-zero: a residency census launch (census_probe) only
-    uint32_t* lb;                    // look-back flags [ntiles * kWaves]
+    uint32_t* lb;                    // look-back flags, one per 64-packet chunk
     uint32_t lb_tag;                 // this launch's flag tag
+    uint32_t tw;                     // chunks per tile (kWaves; fewer for small batches)
+    uint32_t ntiles;                 // tiles of tw chunks
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
@@ -997,8 +998,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // finish ran alone for ~4 us after the first: the CU favours older waves).  Global chunk
     // numbers ascend with k, and a wave's claims ascend.
     auto chunk_of = [&](uint32_t k) -> uint32_t {
-        const uint32_t t = blockIdx.x + (k / (uint32_t)kWaves) * gridDim.x;
-        const uint32_t c = t * (uint32_t)kWaves + k % (uint32_t)kWaves;
+        const uint32_t t = blockIdx.x + (k / a.tw) * gridDim.x;
+        const uint32_t c = t * a.tw + k % a.tw;
         return t < a.ntiles && c * 64u < a.n ? c : kNone;
     };
     if (tid == 0) s_claim = kWaves;
@@ -1096,8 +1097,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (blockIdx.x < a.ntiles) {
         const uint32_t own = (a.ntiles - 1u - blockIdx.x) / gridDim.x + 1u;
         const uint32_t tl = blockIdx.x + (own - 1u) * gridDim.x;
-        const uint32_t lc = min((uint32_t)kWaves, (a.n - tl * (uint32_t)kTile + 63u) / 64u);
-        nloc = (own - 1u) * (uint32_t)kWaves + lc;
+        const uint32_t lc = min(a.tw, (a.n - tl * a.tw * 64u + 63u) / 64u);
+        nloc = (own - 1u) * a.tw + lc;
     }
     auto claim = [&]() {
         uint32_t kn = 0;
@@ -2552,7 +2553,6 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.desc = d_desc;
     a.verdict = d_verdict;
     a.n = (uint32_t)n;
-    a.ntiles = ntiles;
     a.rv4 = c->rv4;
     a.rv6 = c->rv6;
     a.rinfo = c->rinfo;
@@ -2615,7 +2615,15 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, c->tss, emit, lds, s);
     if (grid_cap == 0) return -1;
-    const uint32_t grid = ntiles == 0 ? 1u : ntiles < grid_cap ? ntiles : grid_cap;
+    // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
+    // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
+    // more CUs (a 10k-packet batch on ten CUs, four waves per SIMD, took 9.2 us; spread, 7.9).
+    const uint32_t nchunks = (uint32_t)((n + 63) / 64);
+    uint32_t tw = (uint32_t)kWaves;
+    while (tw > 1 && (nchunks + tw - 1) / tw < grid_cap) tw >>= 1;
+    a.tw = tw;
+    a.ntiles = (nchunks + tw - 1) / tw;
+    const uint32_t grid = a.ntiles == 0 ? 1u : a.ntiles < grid_cap ? a.ntiles : grid_cap;
     launch_classify(c->tss, emit, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
