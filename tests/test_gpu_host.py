@@ -128,3 +128,27 @@ def test_host_roundtrip_permuted_descriptors(gpu_worker_factory, chunk):
                                         "l1": r.l1}, f"permuted chunk={chunk}")
     finally:
         w.close()
+
+
+@pytest.mark.parametrize("case", ["edge_zero", "edge_consistent"])
+@pytest.mark.parametrize("chunk", [100, 0])
+def test_host_roundtrip_edge_frames(gpu_worker_factory, case, chunk):
+    """Edge frames (ARP requests for the port answered in place, NS / NA, every parse gate)
+    through the host round trip: equals the oracle with table writes deferred (the snapshot
+    semantics of upe_gpu_process, as test_gpu_parity's one-segment edge case)."""
+    wl, _ = golden_io.load(case)
+    r = oracle.run_restated(wl, apply_control=False)
+    assert np.count_nonzero(r.verdict & np.uint32(0x40)) > 0, "no ARP reply in the fixture"
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        if case == "edge_consistent":
+            w.set_l1(wl.l1)
+        frames = wl.frames.copy()
+        verdict = np.zeros(wl.n, np.uint32)
+        w.process_host(frames, wl.desc, verdict, chunk)
+        _check(w, wl, frames, verdict, {"verdict": r.verdict, "frames": r.frames,
+                                        "counters": r.counters, "rule_stats": r.rule_stats,
+                                        "l1": r.l1}, f"{case} chunk={chunk}")
+    finally:
+        w.close()
