@@ -1465,7 +1465,7 @@ constexpr uint32_t kHistRange = UPE_HIST_RANGE;   // most rules per workgroup: 1
 constexpr uint32_t kHistChunk = 1u << 24;   // most packets per workgroup
 constexpr uint32_t kHistChunkMin = 8192;
 #ifndef UPE_HIST_TARGET
-#define UPE_HIST_TARGET 1024
+#define UPE_HIST_TARGET 256
 #endif
 constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
 constexpr int kHistBlock = 1024;
@@ -1621,6 +1621,26 @@ int fail(const std::string& msg) {
         if (e_ != hipSuccess)                                                                \
             return fail(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
     } while (0)
+
+// Makes the context's device current for the duration of an ABI call and restores the caller's
+// current device on return (the ABI must not move the calling thread to another device).
+struct DevScope {
+    int prev = -1;
+    hipError_t e;
+    explicit DevScope(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        e = prev == d ? hipSuccess : hipSetDevice(d);
+    }
+    ~DevScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DevScope(const DevScope&) = delete;
+    DevScope& operator=(const DevScope&) = delete;
+};
+#define DEV_SCOPE(dev)                                                                       \
+    DevScope dev_scope_(dev);                                                                \
+    HIP_TRY(dev_scope_.e)
 
 uint32_t act_code(int32_t type) { return type == UPE_ACT_DROP ? 0u : type == UPE_ACT_FWD ? 1u : 2u; }
 uint32_t mac_lo(const uint8_t* m) {
@@ -2018,8 +2038,9 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
         upe_gpu_close(c);
         return nullptr;
     };
+    DevScope dg(device);
     hipError_t e;
-    if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
+    if ((e = dg.e) != hipSuccess) return bad(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return bad(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming)) != hipSuccess)
@@ -2035,7 +2056,7 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
             c->cus = cus;
         if (const char* v = getenv("UPE_GPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = atoi(v);
     }
-    // payload slots for the largest grid a launch uses (8 workgroups of 256 threads per CU)
+    // payload slots for the largest grid a launch uses (at most 8 workgroups per CU)
     c->paycap = 8u * (uint32_t)c->cus;
     if ((e = hipMalloc(&c->pay, 2 * (size_t)c->paycap * sizeof(TilePay))) != hipSuccess)
         return bad(e, "hipMalloc payloads");
@@ -2069,7 +2090,7 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
 
 void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->lens16, c->arp, c->ndp, c->st, c->stats,
                     c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
@@ -2269,7 +2290,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     if (!c) return fail("null context");
     if (count > c->cap) return fail("rule count exceeds the capacity given at open");
     if (count && !rules) return fail("null rules");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
     std::vector<RuleV4> v4(pad);
     std::vector<RuleV6> v6(pad);
@@ -2376,7 +2397,7 @@ int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_
         return fail("neighbour table capacity must be a power of two (arp_table_init)");
     if ((arp_capacity && !arp) || (ndp_capacity && !ndp)) return fail("null table");
     if (arp_capacity > (1u << 30) || ndp_capacity > (1u << 30)) return fail("table too large");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     // Keep only the entries a reference probe reaches (arp_get_mac, src/arp_table.c:55-80:
     // home slot ip & (cap-1), linear probe, first valid match, stop at the first invalid slot).
     std::vector<uint32_t> arp_keep;
@@ -2466,7 +2487,7 @@ int upe_gpu_set_port(upe_gpu_ctx_t* c, const uint8_t eth_addr[6], uint32_t ip4_a
 
 int upe_gpu_set_l1(upe_gpu_ctx_t* c, const upe_l1_state_t* l1) {
     if (!c || !l1) return fail("null argument");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     DevL1 d;
     memset(&d, 0, sizeof d);
     d.arp_ip = l1->last_arp_ip;
@@ -2485,7 +2506,7 @@ int upe_gpu_set_l1(upe_gpu_ctx_t* c, const upe_l1_state_t* l1) {
 
 int upe_gpu_get_l1(upe_gpu_ctx_t* c, upe_l1_state_t* l1) {
     if (!c || !l1) return fail("null argument");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     if (l1_sync(c) != 0) return -1;
     HIP_TRY(hipDeviceSynchronize());
     DevL1 d;
@@ -2527,7 +2548,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         }
         return 0;
     }
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     hipStream_t s = pick(c, stream);
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     if (ensure_scratch(c, ntiles ? ntiles : 1) != 0) return -1;
@@ -2691,7 +2712,7 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
                          const uint64_t* h_desc, uint32_t* h_verdict, size_t n, size_t chunk) {
     if (!c) return fail("null context");
     if (n && (!h_frames || !h_desc || !h_verdict)) return fail("null host buffer");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     if (chunk == 0) chunk = (size_t)1 << 18;
     if (!c->s_in) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
@@ -2835,7 +2856,7 @@ int upe_gpu_compact(upe_gpu_ctx_t* c, const uint32_t* d_verdict, size_t n, uint3
     if (!d_count || (n && (!d_verdict || !d_index))) return fail("null buffer");
     if (n > 0xFFFFFFFFull - kCompactBlock) return fail("n must fit in 32 bits");
     if (code > 15) return fail("verdict code out of range");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     hipStream_t s = pick(c, stream);
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(uint64_t), s));
@@ -2919,7 +2940,7 @@ int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_
     if ((arp_capacity & (arp_capacity - 1)) || (ndp_capacity & (ndp_capacity - 1)))
         return fail("neighbour table capacities must be powers of two");
     if (n == 0) return upe_gpu_process(c, d_frames, d_desc, d_verdict, 0, stream);
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     hipStream_t s = pick(c, stream);
     // 1. mark and list the table-writing control packets, in packet order
     if (n > c->ctrl_alloc) {
@@ -3026,14 +3047,14 @@ int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_
 
 int upe_gpu_sync(upe_gpu_ctx_t* c, void* stream) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipStreamSynchronize(pick(c, stream)));
     return check_lookback(c);
 }
 
 int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
     if (!c || !info) return fail("null argument");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipDeviceSynchronize());
     memset(info, 0, sizeof *info);
     info->first_ctrl = ~0ull;
@@ -3055,7 +3076,7 @@ int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
 int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_t* rule_stats,
                       size_t capacity) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipDeviceSynchronize());
     if (check_lookback(c) != 0) return -1;
     if (counters) {
@@ -3093,7 +3114,7 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
 
 int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     if (order_on(c, c->stream) != 0) return -1;
     HIP_TRY(hipMemsetAsync(&c->st->totals[0], 0, sizeof(c->st->totals), c->stream));
     if (c->k > 0) {   // the last batch's counters, not yet folded into the totals
@@ -3115,7 +3136,7 @@ int upe_gpu_reset_stats(upe_gpu_ctx_t* c) {
 int upe_gpu_timing_span(upe_gpu_ctx_t* c, int every, int span) {
     if (!c) return fail("null context");
     if (span < 1) return fail("span must be at least 1");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipDeviceSynchronize());
     c->ev_used = 0;   // the pool is kept for reuse
     c->timing = every > 0;
@@ -3134,7 +3155,7 @@ int upe_gpu_timing_enable(upe_gpu_ctx_t* c, int enable) {
 int upe_gpu_timing_read(upe_gpu_ctx_t* c, double* classify_ms, double* finalize_ms,
                         uint64_t* launches) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     double a = 0, b = 0;
     for (size_t j = 0; j + 2 <= c->ev_used; j += 2) {
         HIP_TRY(hipEventSynchronize(c->ev[j + 1]));
@@ -3154,7 +3175,8 @@ void* upe_gpu_malloc(upe_gpu_ctx_t* c, size_t bytes) {
         return nullptr;
     }
     void* p = nullptr;
-    if (hipSetDevice(c->device) != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+    DevScope dg(c->device);
+    if (dg.e != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
         fail("hipMalloc failed");
         return nullptr;
     }
@@ -3163,21 +3185,21 @@ void* upe_gpu_malloc(upe_gpu_ctx_t* c, size_t bytes) {
 
 int upe_gpu_free(upe_gpu_ctx_t* c, void* p) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     if (p) HIP_TRY(hipFree(p));
     return 0;
 }
 
 int upe_gpu_memcpy_h2d(upe_gpu_ctx_t* c, void* dst, const void* src, size_t bytes, void* stream) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(c, stream)));
     return 0;
 }
 
 int upe_gpu_memcpy_d2h(upe_gpu_ctx_t* c, void* dst, const void* src, size_t bytes, void* stream) {
     if (!c) return fail("null context");
-    HIP_TRY(hipSetDevice(c->device));
+    DEV_SCOPE(c->device);
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(c, stream)));
     return 0;
 }
