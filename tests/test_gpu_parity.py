@@ -281,14 +281,18 @@ def test_config_d_full_properties(gpu_worker_factory):
 
 
 @pytest.mark.parametrize("emit", [False, True])
-@pytest.mark.parametrize("first_hit", [None, 0, 777, 150_001, 299_999])
-def test_lookback_far_first_hit(gpu_worker_factory, first_hit, emit):
+@pytest.mark.parametrize("n,first_hit", [(300_000, None), (300_000, 0), (300_000, 777),
+                                         (300_000, 150_001), (300_000, 299_999),
+                                         (800_000, None), (800_000, 400_000),
+                                         (800_000, 799_000)])
+def test_lookback_far_first_hit(gpu_worker_factory, n, first_hit, emit):
     """A starting ARP entry that disagrees with the table and a batch aimed at it: every packet
     before the first miss-then-hit packet (placed far into the batch, or absent) must take the
-    entry's MAC — the decoupled look-back across ~1200 tiles."""
+    entry's MAC — the decoupled look-back across ~1200 tiles (and, at 800k packets, across
+    workgroups that own several tiles each)."""
     from upe_amd.layout import desc_offsets
 
-    wl = synth.config_b(n=300_000, seed=12)
+    wl = synth.config_b(n=n, seed=12)
     ip0 = 0x0A800007
     l1 = synth.l1_zero()
     l1["last_arp_ip"] = ip0
