@@ -1106,6 +1106,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         return chunk_of(__builtin_amdgcn_readfirstlane(kn));
     };
     uint32_t chn = kNone;   // this wave's next chunk
+    // The descriptors a wave loads are consumed where they were loaded (this one, and the late
+    // claim's at the end of the loop body), so that no descriptor is still pending at the loop
+    // header: the wait for it would be a vmcnt(0) every iteration shares, which also waits for
+    // the previous chunk's stores.
+    asm volatile("" : "+v"(dsc_next));
     for (bool first = true; ch != kNone; first = false, ch = chn) {
         bool late;
         {
@@ -1375,6 +1380,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             chn = claim();
             dsc_next = 0;
             if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
+            asm volatile("" : "+v"(dsc_next));   // consumed here (see before the loop)
         }
     }
     STAMP(4);
