@@ -218,12 +218,20 @@ struct NeighIndex {
 //   [10] smallest sorted index in the group  [11] log2(slots)  [12] seed  [13] first slot
 //   [14] 1 | action << 8 when every mask word is zero (a catch-all group: every packet of the
 //        family matches its one key, so the probe needs no memory access), else 0
+//   [15] 1 + offset of the group's fingerprints in the staged image (tfs), 0 = not staged
 // Slots: family 4 = 2 x uint4 {k0, k1, s0, d0}, {index, used, -, -};
 //        family 6 = 3 x uint4 {k0, k1, s0, s1}, {s2, s3, d0, d1}, {d2, d3, index, used}.
 struct __attribute__((aligned(16))) TssGroup {
     uint32_t w[16];
 };
 constexpr int kTssSlot4 = 2, kTssSlot6 = 3;   // uint4 per slot
+// Fingerprints of small groups staged in LDS (word [15] of such a group: 1 + its offset in the
+// staged image): their probes then wait for no fingerprint round trip.
+#ifndef UPE_FP_STAGE_MAX
+#define UPE_FP_STAGE_MAX 8192
+#endif
+constexpr uint32_t kFpStageMax = UPE_FP_STAGE_MAX;    // staged fingerprints (2 bytes each)
+constexpr uint32_t kFpStageGroup = 4096;             // largest group (slots) staged
 
 struct Args {
     uint8_t* frames;
@@ -244,6 +252,7 @@ struct Args {
     const uint4* tt6;
     const uint16_t* tf4;           // per slot: 16-bit fingerprint of its key, 0 = empty
     const uint16_t* tf6;
+    const uint4* tfs;              // staged fingerprint image (Args::fp_lds uint4 go to LDS)
     uint32_t ng4, ng6, tss;
     // the context's arrays, passed by value so that no kernel waits on a pointer load
     TilePay* pay;                    // [grid]
@@ -251,6 +260,7 @@ struct Args {
     unsigned long long* stats_idx;   // [kStatReps][nrules_pad][2]
     uint32_t arp_lds;                // ARP index staged in LDS (slots), 0 = read from memory
     uint32_t ndp_lds;                // NDP index staged in LDS (slots, 2 x uint4 each), 0 = not
+    uint32_t fp_lds;                 // staged fingerprints in LDS (uint4 of tfs), 0 = none
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
     uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
@@ -624,7 +634,8 @@ __device__ __forceinline__ uint32_t tss_fmix(uint32_t h) {
 }
 __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, bool is6,
                                                    uint32_t k0, uint32_t k1, const uint32_t s[4],
-                                                   const uint32_t d[4], uint32_t& act) {
+                                                   const uint32_t d[4], uint32_t& act,
+                                                   const uint16_t* sfp) {
     uint32_t best = kNone;
     const uint32_t ng = a.ng4 > a.ng6 ? a.ng4 : a.ng6;
     const uint32_t ngf = is6 ? a.ng6 : a.ng4;
@@ -677,7 +688,18 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
             const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
             const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
             const uint32_t tag = tss_tag(h);
-            const bool m1 = FP[t1] == tag, m2 = FP[t2] == tag;
+            // fingerprints from LDS when the group's are staged, else from memory
+            const uint32_t so = sfp ? (is6 ? q6[15] : q4[15]) : 0u;
+            uint32_t f1, f2;
+            if (so) {
+                const uint32_t b = so - 1u - q[13];
+                f1 = sfp[b + t1];
+                f2 = sfp[b + t2];
+            } else {
+                f1 = FP[t1];
+                f2 = FP[t2];
+            }
+            const bool m1 = f1 == tag, m2 = f2 == tag;
             uint32_t idx = kNone, ac = 0;
             auto probe = [&](uint32_t t) {
                 const uint4 A = T[st * t], B = T[st * t + 1];
@@ -1033,6 +1055,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     uint4* s_ndp = s_arp + a.arp_lds;
     for (uint32_t k = tid; k < a.arp_lds; k += kBlock) s_arp[k] = a.arp.t[k];
     for (uint32_t k = tid; k < 2 * a.ndp_lds; k += kBlock) s_ndp[k] = a.ndp.t[k];
+    uint4* s_fp4 = s_ndp + 2 * a.ndp_lds;
+    if (kTssMode)
+        for (uint32_t k = tid; k < a.fp_lds; k += kBlock) s_fp4[k] = a.tfs[k];
+    const uint16_t* s_fps = kTssMode && a.fp_lds ? reinterpret_cast<const uint16_t*>(s_fp4) : nullptr;
     __syncthreads();
     STAMP(1);
     // The fold itself waits on those loads (and then on at most two payload loads), so it runs
@@ -1211,7 +1237,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             ri = ok ? 0u : kNone;
             act = 1u << 16;
         } else if (kTssMode) {
-            ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act);
+            ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act, s_fps);
         } else {
             if (small_stats)
                 ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
@@ -1719,6 +1745,8 @@ struct upe_gpu_ctx {
     uint4* tt6 = nullptr;
     uint16_t* tf4 = nullptr;
     uint16_t* tf6 = nullptr;
+    uint16_t* tfs = nullptr;          // staged fingerprint image
+    uint32_t nfs = 0;                 // its length in uint4
     uint32_t ng4 = 0, ng6 = 0;
     bool tss = false;
     uint32_t* compact_counts = nullptr;   // upe_gpu_compact: per-block counts
@@ -2099,7 +2127,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->lens16, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->compact_counts,
+                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->tfs,
+                    c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
                     c->hist_part};
     for (void* b : bufs)
@@ -2369,6 +2398,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     // Large tables: a tuple-space index when the rules fall into few mask signatures (one hash
     // probe per signature instead of a test per rule); otherwise the linear scan.
     c->tss = false;
+    c->nfs = 0;
     c->ng4 = c->ng6 = 0;
     const char* force = getenv("UPE_GPU_TSS");   // diagnostic: 0 = never, 1 = always
     if (count > 0 && !(force && force[0] == '0')) {
@@ -2377,6 +2407,19 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             build_tss_family(6, v4, v6, rules, count, f6)) {
             const size_t ng = f4.groups.size() + f6.groups.size();
             if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
+                // the staged fingerprint image: small groups, in probe order, while it fits
+                std::vector<uint16_t> img;
+                for (TssFamily* f : {&f4, &f6})
+                    for (TssGroup& g : f->groups) {
+                        const uint32_t slots = 1u << g.w[11];
+                        if ((g.w[14] & 1u) || slots > kFpStageGroup || img.size() + slots > kFpStageMax)
+                            continue;
+                        g.w[15] = 1u + (uint32_t)img.size();
+                        img.insert(img.end(), f->fp.begin() + g.w[13], f->fp.begin() + g.w[13] + slots);
+                    }
+                img.resize((img.size() + 7) & ~(size_t)7, 0);
+                if (upload(c->tfs, img)) return -1;
+                c->nfs = (uint32_t)(img.size() / 8);
                 if (upload(c->tg4, f4.groups) || upload(c->tg6, f6.groups) ||
                     upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots) ||
                     upload(c->tf4, f4.fp) || upload(c->tf6, f6.fp))
@@ -2596,6 +2639,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.tt6 = c->tt6;
     a.tf4 = c->tf4;
     a.tf6 = c->tf6;
+    a.tfs = reinterpret_cast<const uint4*>(c->tfs);
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
     a.tss = c->tss ? 1u : 0u;
@@ -2638,6 +2682,11 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     if (ndp_slots && ndp_slots <= kNdpLdsSlots && lds + 2 * ndp_slots * sizeof(uint4) <= kLdsDynMax) {
         a.ndp_lds = ndp_slots;
         lds += 2 * ndp_slots * sizeof(uint4);
+    }
+    a.fp_lds = 0u;
+    if (c->tss && c->nfs && lds + c->nfs * sizeof(uint4) <= kLdsDynMax) {
+        a.fp_lds = c->nfs;
+        lds += c->nfs * sizeof(uint4);
     }
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, c->tss, emit, lds, s);
