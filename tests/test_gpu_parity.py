@@ -313,19 +313,21 @@ def test_lookback_far_first_hit(gpu_worker_factory, n, first_hit, emit):
                        "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["0", "1", "1-unstaged"])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
                                   "config_d_small", "edge_inconsistent"])
 def test_rule_index_kinds_agree(gpu_worker_factory, monkeypatch, case, mode):
     """Both classifiers — the linear first-match scan and the tuple-space index — forced on
     every fixture (version-0 rules, mixed v4/v6 masks, wildcard fields, catch-alls) give the
-    reference's first match."""
-    monkeypatch.setenv("UPE_GPU_TSS", mode)
+    reference's first match; the tuple-space probes both with small groups' fingerprints in LDS
+    and with none staged (every group probed slot by slot)."""
+    monkeypatch.setenv("UPE_GPU_TSS", mode[0])
+    monkeypatch.setenv("UPE_GPU_FP_STAGE", "0" if mode.endswith("unstaged") else "1")
     wl, ref = golden_io.load(case)
     w = gpu_worker_factory(wl.capacity)
     try:
         w.configure(wl)
-        assert w.rule_index_kind() == int(mode)
+        assert w.rule_index_kind() == int(mode[0])
         frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w)
     finally:
         w.close()

@@ -232,6 +232,18 @@ constexpr int kTssSlot4 = 2, kTssSlot6 = 3;   // uint4 per slot
 #endif
 constexpr uint32_t kFpStageMax = UPE_FP_STAGE_MAX;    // staged fingerprints (2 bytes each)
 constexpr uint32_t kFpStageGroup = 4096;             // largest group (slots) staged
+// Groups whose fingerprints are not staged are probed without them: slot t1 (where cuckoo
+// placement leaves ~80 % of the keys at this load), then t2 if t1 holds another key.  One round
+// trip for most hits instead of a fingerprint trip followed by a slot trip (config D 808 -> 775
+// us); a miss takes two slot reads.
+#ifndef UPE_TSS_DIRECT
+#define UPE_TSS_DIRECT 1
+#endif
+constexpr bool kTssDirect = UPE_TSS_DIRECT;
+#ifndef UPE_TSS_RATIO_X2
+#define UPE_TSS_RATIO_X2 5
+#endif
+constexpr uint32_t kTssRatioX2 = UPE_TSS_RATIO_X2;   // tuple-space slots >= ratio / 2 x keys
 
 struct Args {
     uint8_t* frames;
@@ -695,6 +707,8 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
                 const uint32_t b = so - 1u - q[13];
                 f1 = sfp[b + t1];
                 f2 = sfp[b + t2];
+            } else if (kTssDirect) {
+                f1 = f2 = tag;   // no fingerprints: slot t1, then t2
             } else {
                 f1 = FP[t1];
                 f2 = FP[t2];
@@ -1814,7 +1828,8 @@ NeighIndex ndp_index(const upe_gpu_ctx* c) { return NeighIndex{c->ndp, c->ndp_bi
 // share a hash key, the device compares the full address).  Starts at 2^bits >= 2.5 n slots and
 // tries seeds, then doubles, until every key sits in slot1 or slot2.  bits = 0 for no keys.
 template <class H>
-int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot);
+int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot,
+                    uint32_t ratio_x2 = 5);
 
 int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& seed,
                  std::vector<int32_t>& slot) {
@@ -1824,14 +1839,15 @@ int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& see
 
 // Same, with a seed-dependent 32-bit hash per key: hfn(j, seed).
 template <class H>
-int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot) {
+int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot,
+                    uint32_t ratio_x2) {
     std::vector<uint32_t> key(n);
     slot.clear();
     bits = 0;
     seed = 0;
     if (n == 0) return 0;
     bits = 1;
-    while (((size_t)1 << bits) * 2 < n * 5) ++bits;
+    while (((size_t)1 << bits) * 2 < n * ratio_x2) ++bits;
     for (; bits <= 31; ++bits) {
         const size_t m = (size_t)1 << bits;
         for (uint32_t attempt = 0; attempt < 64; ++attempt) {
@@ -2264,7 +2280,7 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
         std::vector<int32_t> slot;
         if (cuckoo_place_fn(keys.size(),
                             [&](size_t j, uint32_t sd) { return tss_hash(keys[j].data(), nw, sd); },
-                            bits, seed, slot) != 0)
+                            bits, seed, slot, kTssRatioX2) != 0)
             return false;
         TssGroup d;
         memset(&d, 0, sizeof d);
@@ -2409,8 +2425,10 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
                 // the staged fingerprint image: small groups, in probe order, while it fits
                 std::vector<uint16_t> img;
+                const char* fps = getenv("UPE_GPU_FP_STAGE");   // diagnostic: 0 = stage none
                 for (TssFamily* f : {&f4, &f6})
                     for (TssGroup& g : f->groups) {
+                        if (fps && fps[0] == '0') break;
                         const uint32_t slots = 1u << g.w[11];
                         if ((g.w[14] & 1u) || slots > kFpStageGroup || img.size() + slots > kFpStageMax)
                             continue;
