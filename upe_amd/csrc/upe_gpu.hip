@@ -1500,9 +1500,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // at most 2^24 packets of at most 65535 bytes), then writes the bins densely into per-chunk
 // partials that upe_hist_reduce sums (device atomics per nonzero bin, measured in round 2, were
 // no faster and needed a packed staging array).  Every range re-reads its chunk (verdict word + the 2-byte length the classify
-// pass left), so ranges are as wide as LDS allows; 1024-thread workgroups with eight packets per
-// thread per round keep enough loads in flight (config D: 256-thread workgroups with four packets
-// a round spent ~300 us per 16M batch waiting on them).
+// pass left), so ranges are as wide as LDS allows; 1024-thread workgroups with sixteen packets
+// per thread per round keep enough loads in flight (config D: 256-thread workgroups with four
+// packets a round spent ~300 us per 16M batch waiting on them; eight a round 69.5 us, sixteen
+// 62.6 us, thirty-two slower again).
 // ------------------------------------------------------------------------------------------
 #ifndef UPE_HIST_RANGE
 #define UPE_HIST_RANGE 16384
@@ -1515,6 +1516,11 @@ constexpr uint32_t kHistChunkMin = 8192;
 #endif
 constexpr uint32_t kHistTarget = UPE_HIST_TARGET;   // workgroups per group-by launch
 constexpr int kHistBlock = 1024;
+#ifndef UPE_HIST_PER
+#define UPE_HIST_PER 16
+#endif
+constexpr int kHistPer = UPE_HIST_PER;   // packets per thread per round (a multiple of 8)
+static_assert(kHistPer % 8 == 0 && 8192 % (kHistPer * 1) == 0, "group-by rounds stay 16-byte aligned");
 
 __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verdict,
                                                             const uint16_t* lens, uint32_t n,
@@ -1527,27 +1533,34 @@ __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verd
     for (uint32_t k = threadIdx.x; k < range; k += kHistBlock) h[k] = 0;
     __syncthreads();
     const uint32_t pend = n - p0 < chunk ? n : p0 + chunk;
-    // eight packets per thread per round: two 16-byte verdict loads and one 16-byte length load
-    // (chunks start at multiples of 8192, so full groups are 16-byte aligned)
-    for (uint32_t i = p0 + 8 * threadIdx.x; i < pend; i += 8 * kHistBlock) {
-        uint32_t v[8], len[8];
-        if (i + 8 <= pend) {
-            const uint4 a0 = *reinterpret_cast<const uint4*>(verdict + i);
-            const uint4 a1 = *reinterpret_cast<const uint4*>(verdict + i + 4);
-            const uint4 l = *reinterpret_cast<const uint4*>(lens + i);
-            v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
-            v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
-            len[0] = l.x & 0xFFFFu; len[1] = l.x >> 16; len[2] = l.y & 0xFFFFu; len[3] = l.y >> 16;
-            len[4] = l.z & 0xFFFFu; len[5] = l.z >> 16; len[6] = l.w & 0xFFFFu; len[7] = l.w >> 16;
+    // kHistPer packets per thread per round: kHistPer / 4 16-byte verdict loads and kHistPer / 8
+    // 16-byte length loads, all issued before the first bin update (chunks start at multiples of
+    // 8192, so full groups are 16-byte aligned)
+    for (uint32_t i = p0 + kHistPer * threadIdx.x; i < pend; i += kHistPer * kHistBlock) {
+        uint32_t v[kHistPer], len[kHistPer];
+        if (i + kHistPer <= pend) {
+#pragma unroll
+            for (int q = 0; q < kHistPer / 4; ++q) {
+                const uint4 a0 = *reinterpret_cast<const uint4*>(verdict + i + 4 * q);
+                v[4 * q + 0] = a0.x; v[4 * q + 1] = a0.y; v[4 * q + 2] = a0.z; v[4 * q + 3] = a0.w;
+            }
+#pragma unroll
+            for (int q = 0; q < kHistPer / 8; ++q) {
+                const uint4 l = *reinterpret_cast<const uint4*>(lens + i + 8 * q);
+                len[8 * q + 0] = l.x & 0xFFFFu; len[8 * q + 1] = l.x >> 16;
+                len[8 * q + 2] = l.y & 0xFFFFu; len[8 * q + 3] = l.y >> 16;
+                len[8 * q + 4] = l.z & 0xFFFFu; len[8 * q + 5] = l.z >> 16;
+                len[8 * q + 6] = l.w & 0xFFFFu; len[8 * q + 7] = l.w >> 16;
+            }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < kHistPer; ++j) {
                 v[j] = i + j < pend ? verdict[i + j] : 0u;
                 len[j] = i + j < pend ? (uint32_t)lens[i + j] : 0u;
             }
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < kHistPer; ++j) {
             const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
             if (rb != 0 && rb - 1u - r0 < range) atomicAdd(&h[rb - 1u - r0], (1ull << 40) | len[j]);
         }
