@@ -5,7 +5,9 @@ classify launch, plus the rule_stats group-by for tables over 4096 rules) over o
 resident in HBM.  The default output mode is emit (include/upe_gpu.h): verdicts plus one 16-byte
 rewritten-header record per packet, frames read only; --mode inplace rewrites the frames in place
 as upe_gpu_process does, and the JSON line carries the other mode's rate too ("other_mode").  At N=1 the workload is BASELINE.json configs[1] (config B: 1M x 64 B UDP/IPv4, 8 rules);
---config A / C / D run the other configurations.  Every step gets its own pristine copy of the
+--config A / C / D run the other configurations.  A config-B run also times the IMIX workload
+(config C) after the main region, on every rank, and reports it as "imix" (not `value`), so that
+the 64 B and IMIX rates come out of the same run at each GPU count.  Every step gets its own pristine copy of the
 batch (the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the
 work), which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
 
@@ -224,6 +226,72 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
             "windows": windows, "chunk": chunk or (1 << 18), "reps": reps}
 
 
+def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
+             copies_cap: int) -> dict:
+    """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
+    timed the same way as `value`, on every rank at once after the main region, so that a
+    multi-GPU run reports the 64 B and the IMIX rates at each N (BASELINE north_star).  Each rank
+    takes its own shard (seed 3 + 1000 * rank); `copies_cap` distinct copies of the batch
+    (32 x 373 MB, past the Infinity Cache) are cycled.  Not `value`."""
+    from upe_amd import gpu, shard, synth
+
+    wl = synth.config_c(seed=3 + 1000 * rank)
+    n = wl.n
+    worker = gpu.GpuWorker(local, wl.capacity)
+    worker.configure(wl)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    fbytes = int(wl.frames.nbytes)
+    stride = (fbytes + 255) // 256 * 256
+    copies = max(2, min(steps + warmup, copies_cap))
+    pristine = torch.from_numpy(wl.frames).to(dev)
+    pool = torch.empty(copies * stride, dtype=torch.uint8, device=dev)
+    for c in range(copies):
+        pool[c * stride: c * stride + fbytes].copy_(pristine)
+    del pristine
+    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    base = pool.data_ptr()
+
+    def run(k0: int, count: int) -> None:
+        ptrs = [base + (k % copies) * stride for k in range(k0, k0 + count)]
+        if mode == "emit":
+            worker.process_batches_emit(ptrs, desc, verdict, hdr, n, sh)
+        else:
+            worker.process_batches(ptrs, desc, verdict, n, sh)
+
+    run(0, warmup)
+    torch.cuda.synchronize(dev)
+    worker.timing_span(EVENT_EVERY, EVENT_SPAN)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(warmup, steps)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    total = float(shard.sum_over_ranks([n * steps], dist, dev)[0])
+    v = verdict.cpu().numpy().view(np.uint32).copy()
+    cms, _, launches = worker.timing_read()
+    worker.close()
+    del pool, desc, verdict, hdr
+    bpp = algorithmic_bytes(wl, v, emit=mode == "emit")
+    kern_s = cms / launches / 1e3 if launches else float("nan")
+    achieved = float(bpp.sum()) / kern_s / 1e9
+    return {"workload": WORKLOADS["C"], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
+            "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps,
+            "packets_per_gpu_step": n,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "kernel_ms": round(kern_s * 1e3, 5),
+                         "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
+                         "traffic": pmc_traffic("C", n, mode)},
+            "what": f"all ranks at once after the main region, {copies} distinct batch copies "
+                    "cycled, same timing protocol as value (barrier, max over ranks)"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,6 +318,10 @@ def main() -> None:
                          " inplace: frames rewritten in place (upe_gpu_process)")
     ap.add_argument("--no-other-mode", action="store_true",
                     help="skip timing the other output mode after the timed region")
+    ap.add_argument("--no-imix", action="store_true",
+                    help="skip the IMIX leg (config C timed after the main region on every rank, "
+                         "reported as \"imix\" beside value; config B runs only)")
+    ap.add_argument("--imix-copies", type=int, default=32)
     args = ap.parse_args()
 
     import torch
@@ -373,6 +445,10 @@ def main() -> None:
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
                                     args.workers_per_gpu, args.steps)
+    imix = None
+    if args.config == "B" and not args.no_imix and not args.packets:
+        imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
+                        args.imix_copies)
     probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
@@ -448,6 +524,8 @@ def main() -> None:
         }
         if other:
             out["other_mode"] = other
+        if imix:
+            out["imix"] = imix
         if shared:
             out["workers_sharing_gpu"] = shared
         if hr:

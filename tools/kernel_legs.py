@@ -1,0 +1,47 @@
+"""Split a rocprofv3 kernel trace of one bench.py run into its legs and summarise each.
+
+A default config-B bench run launches the same classify instantiation for two workloads: the
+64 B batches of `value` and, after the other-mode leg, the IMIX batches of the "imix" field.
+rocprofv3's --stats table averages them together; this splits the dispatches of each kernel
+into legs at gaps longer than --gap-ms (the IMIX leg starts after its batch is generated on the
+host, seconds later) and prints count / mean / min / max per leg, so that each leg's mean can
+be set beside the bench line's kernel_ms.
+
+Usage: python tools/kernel_legs.py <p_kernel_trace.csv> [--gap-ms 50] [--match upe_]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import statistics
+
+
+def legs(path: str, gap_ms: float, match: str):
+    rows = [r for r in csv.DictReader(open(path)) if match in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    by_name: dict[str, list[list[tuple[int, int]]]] = {}
+    for r in rows:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        segs = by_name.setdefault(r["Kernel_Name"], [])
+        if not segs or s - segs[-1][-1][1] > gap_ms * 1e6:
+            segs.append([])
+        segs[-1].append((s, e))
+    return by_name
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--gap-ms", type=float, default=50.0)
+    ap.add_argument("--match", default="upe_")
+    a = ap.parse_args()
+    print(f"{'kernel':70s} {'leg':>3s} {'calls':>6s} {'mean_us':>9s} {'min_us':>9s} {'max_us':>9s}")
+    for name, segs in legs(a.trace, a.gap_ms, a.match).items():
+        for i, seg in enumerate(segs):
+            d = [(e - s) / 1e3 for s, e in seg]
+            print(f"{name[:70]:70s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
+                  f"{min(d):9.2f} {max(d):9.2f}")
+
+
+if __name__ == "__main__":
+    main()
