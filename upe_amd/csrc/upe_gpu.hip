@@ -92,6 +92,13 @@ constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (s
 #define UPE_LATE_CLAIM 16
 #endif
 constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
+// Issue the next chunk's window loads in the middle of the current chunk (after its rule
+// match), so that they fly during the rest of it: bit 0 emit-mode linear-scan kernel, bit 1 also
+// the in-place one (config B emit 26.2 -> 25.4 us per 1M batch; C unchanged; in place +0.3 %
+// with a VGPR spilled, so off; issued right after the parse instead: B no gain, C 39.0 -> 40.5).
+#ifndef UPE_MID_PREFETCH
+#define UPE_MID_PREFETCH 1
+#endif
 // Neighbour indexes staged in LDS (one workgroup per CU, so a CU reads them once per launch):
 // ARP up to 2048 slots (32 KB), NDP up to 2048 slots (64 KB), within kLdsDynMax of dynamic LDS.
 #ifndef UPE_ARP_LDS_SLOTS
@@ -1026,6 +1033,26 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
         }
     };
+    // The next chunk's window issued in the middle of the current chunk (after its rule match),
+    // so that its loads fly during the rest of it: into named registers carried into the next
+    // iteration (not an array the compiler might place in scratch).  Only the linear-scan
+    // kernels: the tuple-space ones have no registers to spare.
+    constexpr bool kMid = (UPE_MID_PREFETCH & 1) && !kTssMode && (kEmit || (UPE_MID_PREFETCH & 2));
+    struct Win { uint4 c0, c1, c2, c3, c4; };
+    auto fetch_window = [&](uint64_t dsc, bool live) -> Win {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        Win v{z, z, z, z, z};
+        if (live) {
+            const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
+            const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
+            v.c0 = q[0]; v.c1 = q[1]; v.c2 = q[2];
+            if (len > 48u) v.c3 = q[3];
+            if (len > 64u) v.c4 = q[4];
+        }
+        return v;
+    };
+    Win nw;
+    bool have_nw = false;   // nw holds the window of the wave's next chunk
     // Work: the workgroup owns tiles blockIdx, blockIdx + grid, ... (one per CU at a time, so a
     // CU's tiles are one workgroup's), and each wave takes 64-packet chunks of them in order:
     // workgroup-local chunk k is chunk k % kWaves of the workgroup's tile k / kWaves.  Waves
@@ -1168,7 +1195,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint32_t off16 = (uint32_t)(dsc >> 20);
         uint8_t* p = a.frames + ((size_t)off16 << 4);
         uint32_t w[20];
-        load_window(dsc, live, w);
+        if (kMid && have_nw) {
+            const uint4 c[5] = {nw.c0, nw.c1, nw.c2, nw.c3, nw.c4};
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                w[4 * j + 0] = c[j].x; w[4 * j + 1] = c[j].y; w[4 * j + 2] = c[j].z; w[4 * j + 3] = c[j].w;
+            }
+        } else {
+            load_window(dsc, live, w);
+        }
+        have_nw = false;
         dsc_next = 0;
         if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
         if (!folded) fold_start();
@@ -1280,6 +1316,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
         uint32_t flags = r.flags;
         if (first) STAMP_VM(3);
+        // the next chunk's window (its descriptor has been back since early in this chunk):
+        // issued here, it arrives while this chunk finishes
+        if (kMid && chn != kNone) {
+            nw = fetch_window(dsc_next, chn * 64u + (uint32_t)lane < a.n);
+            have_nw = true;
+        }
 
         // ---- L3 forward (src/worker.c:155-244) ----
         bool fp4 = false, fp6 = false;       // this packet misses the start entry, hits table
