@@ -7,7 +7,7 @@ mkdir -p gpurun_out/vb
 for spec in "$@"; do
   label=${spec%%=*}; envs=${spec#*=}
   [ "$envs" = "$spec" ] && envs=""
-  timeout -k 10 120 env UPE_GPU_VERBOSE=1 ${envs//,/ } python bench.py --no-cpu-baseline --no-hbm-probe --no-other-mode \
+  timeout -k 10 120 env UPE_GPU_VERBOSE=1 ${envs//,/ } python bench.py --no-cpu-baseline --no-hbm-probe --no-other-mode --no-imix \
       --mode ${MODE:-emit} ${BENCH_ARGS:-} > gpurun_out/vb/$label.json 2> gpurun_out/vb/$label.err
   rc=$?
   python - "$label" "$rc" <<'PY'
