@@ -94,8 +94,9 @@ constexpr int kStatReps = 8;   // replicas of the per-sorted-index rule_stats (s
 constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 // Issue the next chunk's window loads in the middle of the current chunk (after its rule
 // match), so that they fly during the rest of it: bit 0 emit-mode linear-scan kernel, bit 1 also
-// the in-place one (config B emit 26.2 -> 25.4 us per 1M batch; C unchanged; in place +0.3 %
-// with a VGPR spilled, so off; issued right after the parse instead: B no gain, C 39.0 -> 40.5).
+// the in-place one, bit 2 also the tuple-space ones (config B emit 26.2 -> 25.4 us per 1M batch;
+// C unchanged; in place +0.3 % with a VGPR spilled, so off; tuple space: D unchanged, with twice
+// the SGPR spills, so off; issued right after the parse instead: B no gain, C 39.0 -> 40.5).
 #ifndef UPE_MID_PREFETCH
 #define UPE_MID_PREFETCH 1
 #endif
@@ -1037,7 +1038,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // so that its loads fly during the rest of it: into named registers carried into the next
     // iteration (not an array the compiler might place in scratch).  Only the linear-scan
     // kernels: the tuple-space ones have no registers to spare.
-    constexpr bool kMid = (UPE_MID_PREFETCH & 1) && !kTssMode && (kEmit || (UPE_MID_PREFETCH & 2));
+    constexpr bool kMid = (UPE_MID_PREFETCH & 1) && (!kTssMode || (UPE_MID_PREFETCH & 4)) &&
+                          (kEmit || (UPE_MID_PREFETCH & 2));
     struct Win { uint4 c0, c1, c2, c3, c4; };
     auto fetch_window = [&](uint64_t dsc, bool live) -> Win {
         const uint4 z = make_uint4(0, 0, 0, 0);
