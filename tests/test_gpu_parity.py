@@ -191,6 +191,23 @@ def test_random_l1_starts(gpu_worker_factory, emit):
         assert np.count_nonzero(r.verdict & 0x80) > 0
 
 
+@pytest.mark.parametrize("emit", [False, True])
+@pytest.mark.parametrize("config", ["B", "C"])
+def test_ragged_batch_sizes(gpu_worker_factory, config, emit):
+    """Batch sizes around every boundary of the work split: a single packet, a partial first
+    chunk, one chunk plus one packet, batches too small to give every resident workgroup a
+    full tile (narrow tiles), a partial last tile and a partial last chunk of a large batch —
+    each against the oracle, so the chunk claims, late claims and the window prefetch of the
+    next chunk are exact at every edge."""
+    make = synth.config_b if config == "B" else synth.config_c
+    for n in (1, 63, 65, 1000, 16385, 262145):
+        wl = make(n=n, seed=70 + n % 97)
+        r = oracle.run_restated(wl)
+        got = _run(gpu_worker_factory, wl, emit=emit)
+        _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
+                           "rule_stats": r.rule_stats, "l1": r.l1}, f"{config} n={n}")
+
+
 def test_empty_batch(gpu_worker_factory):
     wl, _ = golden_io.load("config_b_small")
     w = gpu_worker_factory(wl.capacity)
