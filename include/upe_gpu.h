@@ -328,8 +328,9 @@ int upe_gpu_get_stats(upe_gpu_ctx_t *ctx, upe_counters_t *counters, upe_rule_sta
                       size_t capacity);
 int upe_gpu_reset_stats(upe_gpu_ctx_t *ctx);
 
-/* Kernel timing.  enable = k > 0: every k-th upe_gpu_process() call (the first, then every k-th)
- * records HIP events on its stream around its launches (classify, plus the rule_stats group-by
+/* Kernel timing.  enable = k > 0: every k-th upe_gpu_process() call (calls k/2, k/2 + k, ...
+ * after enabling: not the first, which starts from an idle queue) records HIP events on its
+ * stream around its launches (classify, plus the rule_stats group-by
  * pass of tables over 4096 rules); sampling keeps the events' own queue cost out of a throughput
  * run.  enable = 0 turns timing off.  upe_gpu_timing_span(ctx, every, span): each sample's
  * event pair brackets `span` consecutive calls instead of one, so the events' own latency is

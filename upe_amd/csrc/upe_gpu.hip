@@ -1856,6 +1856,7 @@ struct upe_gpu_ctx {
     // kernel timing (upe_gpu_timing_*)
     bool timing = false;
     uint32_t timing_every = 1, timing_calls = 0;   // sample every n-th process() call
+    uint32_t timing_phase = 0;     // samples open at calls c with c % timing_every == phase
     uint32_t timing_span = 1;      // calls one sample's event pair brackets
     uint32_t t_left = 0;           // calls left in the open sample (0: none open)
     uint64_t timing_launches = 0;  // calls covered by closed samples
@@ -2681,7 +2682,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     if (order_on(c, s) != 0) return -1;
     // timing sample: an event pair around `timing_span` consecutive calls, opened on every
     // timing_every-th call (samples never overlap)
-    const bool open = c->timing && c->t_left == 0 && (c->timing_calls % c->timing_every) == 0;
+    const bool open = c->timing && c->t_left == 0 &&
+                      (c->timing_calls % c->timing_every) == c->timing_phase;
     if (c->timing) ++c->timing_calls;
     if (open) {
         while (c->ev.size() < c->ev_used + 2) {
@@ -3271,6 +3273,7 @@ int upe_gpu_timing_span(upe_gpu_ctx_t* c, int every, int span) {
     c->ev_used = 0;   // the pool is kept for reuse
     c->timing = every > 0;
     c->timing_every = every > 0 ? (uint32_t)every : 1u;
+    c->timing_phase = c->timing_every / 2;   // not the first call: it starts from an idle queue
     c->timing_span = (uint32_t)span;
     c->timing_calls = 0;
     c->t_left = 0;

@@ -200,9 +200,17 @@ class GpuWorker:
                                         _dev_ptr(verdict), _dev_ptr(hdr), n, stream or None),
                "upe_gpu_process_emit")
 
+    @staticmethod
+    def frames_list(frames_ptrs):
+        """A native array of batch pointers for process_batches[_emit] (build it once, outside a
+        timed region, and pass it instead of a Python list)."""
+        if isinstance(frames_ptrs, ctypes.Array):
+            return frames_ptrs
+        return (ctypes.c_void_p * len(frames_ptrs))(*[int(x) for x in frames_ptrs])
+
     def process_batches_emit(self, frames_ptrs, desc, verdict, hdr, n: int, stream=None) -> None:
         """process_batches in emit mode (every batch writes its records to `hdr`)."""
-        arr = (ctypes.c_void_p * len(frames_ptrs))(*[int(x) for x in frames_ptrs])
+        arr = self.frames_list(frames_ptrs)
         _check(LIB.upe_gpu_process_batches_emit(self._ctx, arr, _dev_ptr(desc), _dev_ptr(verdict),
                                                 _dev_ptr(hdr), n, len(frames_ptrs),
                                                 stream or None),
@@ -210,7 +218,7 @@ class GpuWorker:
 
     def process_batches(self, frames_ptrs, desc, verdict, n: int, stream=None) -> None:
         """Queue len(frames_ptrs) batches (device pointers) back to back from native code."""
-        arr = (ctypes.c_void_p * len(frames_ptrs))(*[int(x) for x in frames_ptrs])
+        arr = self.frames_list(frames_ptrs)
         _check(LIB.upe_gpu_process_batches(self._ctx, arr, _dev_ptr(desc), _dev_ptr(verdict), n,
                                            len(frames_ptrs), stream or None),
                "upe_gpu_process_batches")
