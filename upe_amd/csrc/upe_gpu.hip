@@ -30,7 +30,8 @@
 // One launch per batch, one persistent 1024-thread workgroup per CU (the grid is what a
 // residency census finds the chip holds at once).  Workgroup b owns 1024-packet tiles b,
 // b + grid, ...; its 16 waves claim the tiles' 64-packet chunks from an LDS counter, so they
-// finish together.  Counters, the rule_stats histogram and the L1 bookkeeping accumulate in LDS
+// finish together.  A wave loads its next chunk's descriptors as it starts a chunk and (emit
+// mode) issues that chunk's window loads halfway through, after the rule match.  Counters, the rule_stats histogram and the L1 bookkeeping accumulate in LDS
 // (ballots per chunk) and leave once per workgroup, as one device-atomic instruction per kind,
 // into replicated per-batch accumulators.  Nothing waits for anything at the end of a launch:
 // the next launch folds this batch's accumulators (lazy fold), the host reads them after a
