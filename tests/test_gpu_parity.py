@@ -208,6 +208,19 @@ def test_ragged_batch_sizes(gpu_worker_factory, config, emit):
                            "rule_stats": r.rule_stats, "l1": r.l1}, f"{config} n={n}")
 
 
+@pytest.mark.parametrize("emit", [False, True])
+def test_line_aligned_layout(gpu_worker_factory, monkeypatch, emit):
+    """Config C at 1M with every header window inside one 128-byte line (frames of up to 64
+    bytes on 64-byte boundaries, longer ones on 128-byte boundaries): the layout changes only
+    where frames sit, so the results equal the oracle's on the same batch."""
+    monkeypatch.setenv("UPE_SYNTH_LAYOUT", "line")
+    wl = synth.config_c()
+    r = oracle.run_restated(wl)
+    got = _run(gpu_worker_factory, wl, emit=emit)
+    _assert_same(got, {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
+                       "rule_stats": r.rule_stats, "l1": r.l1}, "C line-aligned")
+
+
 def test_empty_batch(gpu_worker_factory):
     wl, _ = golden_io.load("config_b_small")
     w = gpu_worker_factory(wl.capacity)

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import dataclasses
 
+import os
+
 import numpy as np
 
 from .layout import (ACT_DROP, ACT_FWD, ARP_DTYPE, FRAME_TAIL, HDR_WINDOW, NDP_DTYPE,
@@ -203,7 +205,7 @@ def ipv4_header_checksum(h: np.ndarray, ihl: np.ndarray) -> np.ndarray:
 
 
 def pack_frames(hdr: np.ndarray, lens: np.ndarray, stride: int | None = None,
-                align: int = 16) -> tuple[np.ndarray, np.ndarray]:
+                align: int = 16, line_aligned: bool = False) -> tuple[np.ndarray, np.ndarray]:
     """Pack header rows (first hdr.shape[1] bytes of each frame; the rest of a frame is zero
     payload) into one buffer.  Fixed `stride` or variable (len rounded up to `align`)."""
     n, w = hdr.shape
@@ -213,6 +215,19 @@ def pack_frames(hdr: np.ndarray, lens: np.ndarray, stride: int | None = None,
             raise ValueError("frame longer than stride")
         offs = np.arange(n, dtype=np.int64) * stride
         total = n * stride
+    elif line_aligned:
+        # every frame's header window inside one 128-byte line: frames of up to 64 bytes start
+        # on a 64-byte boundary, longer ones on a 128-byte boundary
+        sizes = np.maximum((lens + 15) // 16 * 16, 16)
+        aligns = np.where(lens <= 64, 64, 128)
+        offs = np.zeros(n, dtype=np.int64)
+        end = 0
+        for i in range(n):
+            a = int(aligns[i])
+            o = (end + a - 1) // a * a
+            offs[i] = o
+            end = o + int(sizes[i])
+        total = end
     else:
         sizes = (lens + align - 1) // align * align
         sizes = np.maximum(sizes, align)
@@ -479,7 +494,8 @@ def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024) -> Workload:
                dst16=v6_dst[rng.integers(0, n_hosts, size=len(r6))], nh=p6,
                hop=rng.integers(1, 129, size=len(r6)), payload_len=size[r6] - 54,
                sport=sport[r6], dport=dport[r6], tcp_doff=np.full(len(r6), 5))
-    frames, desc = pack_frames(h, size)
+    frames, desc = pack_frames(h, size,
+                               line_aligned=os.environ.get("UPE_SYNTH_LAYOUT") == "line")
     return Workload("C", frames, desc, rules, n_rules, arp, ndp)
 
 
