@@ -6,19 +6,27 @@ coalesced read, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-byte 
 Both counters are in KB per dispatch (summed over the counter instances)."""
 import collections
 import csv
+import re
 import glob
 import json
 import sys
 
+
+def _emit_arg(name: str):
+    m = re.search(r"upe_classify<(\w+), (\w+)", name)
+    return m.group(2) if m else None
+
+
 cfg = sys.argv[1] if len(sys.argv) > 1 else "B"
 packets = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 mode = sys.argv[3] if len(sys.argv) > 3 else "emit"      # emit | inplace
-tag = "true>" if mode == "emit" else "false>"             # upe_classify<tss, emit>
+# upe_classify<tss, emit[, lean]>: the second template argument says emit mode
+want = "true" if mode == "emit" else "false"
 vals = {}
 for name in ("fetch", "write"):
     f = glob.glob(f"gpurun_out/pmc_{cfg}_{mode}/{name}/p_counter_collection.csv")[0]
     rows = [r for r in csv.DictReader(open(f))
-            if "upe_classify" in r["Kernel_Name"] and tag in r["Kernel_Name"]]
+            if _emit_arg(r["Kernel_Name"]) == want]
     # only the full-batch launches (the bench's host leg launches smaller chunks)
     gmax = max(int(r["Grid_Size"]) for r in rows)
     acc = collections.defaultdict(float)
