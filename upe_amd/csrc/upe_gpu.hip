@@ -990,9 +990,9 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kEmit: the rewritten header bytes of forwarded packets go to a record per packet (a.hdr,
 // upe_hdr_rec_t, one coalesced 16-byte store per lane) and the frames are only read; otherwise
 // frames are rewritten in place (bytes 0..31 of each forwarded frame).
-// kLean (emit mode, linear scan only): the launch has no flow_hash output, no length side array
-// and every non-empty neighbour index staged in LDS, so those paths are not compiled in (fewer
-// live kernel arguments: config B/C emit kernels spill 70 SGPRs instead of 96, ~1 % faster).
+// kLean (linear scan only): the launch has no flow_hash output, no length side array and every
+// non-empty neighbour index staged in LDS, so those paths are not compiled in (fewer live kernel
+// arguments: config B/C emit kernels spill 70 SGPRs instead of 96, ~1 % faster).
 template <bool kTssMode, bool kEmit, bool kLean = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
@@ -2037,10 +2037,12 @@ int check_lookback(upe_gpu_ctx* c) {
     return 0;
 }
 
-// Kernel variants: bit 1 tuple space, bit 0 emit; kVarLean the lean emit kernel.
-constexpr int kVarLean = 4;
+// Kernel variants: bit 1 tuple space, bit 0 emit; kVarLean / kVarLeanInPlace the lean
+// linear-scan kernels.
+constexpr int kVarLean = 4, kVarLeanInPlace = 5;
 int classify_var(bool tss, bool emit, bool lean) {
-    return lean && emit && !tss ? kVarLean : (tss ? 2 : 0) | (emit ? 1 : 0);
+    if (lean && !tss) return emit ? kVarLean : kVarLeanInPlace;
+    return (tss ? 2 : 0) | (emit ? 1 : 0);
 }
 
 void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
@@ -2060,6 +2062,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, true, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, false, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
     }
     switch (var) {
     case 3: hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
@@ -2067,6 +2071,9 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
     case 1: hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
     case kVarLean:
         hipLaunchKernelGGL((upe_classify<false, true, true>), dim3(grid), dim3(kBlock), lds, s, a);
+        break;
+    case kVarLeanInPlace:
+        hipLaunchKernelGGL((upe_classify<false, false, true>), dim3(grid), dim3(kBlock), lds, s, a);
         break;
     default: hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
     }
@@ -2086,6 +2093,9 @@ uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
     case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true>, kBlock, lds); break;
     case kVarLean:
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true, true>, kBlock, lds);
+        break;
+    case kVarLeanInPlace:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false, true>, kBlock, lds);
         break;
     default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false>, kBlock, lds);
     }
