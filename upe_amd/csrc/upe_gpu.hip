@@ -990,8 +990,8 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kEmit: the rewritten header bytes of forwarded packets go to a record per packet (a.hdr,
 // upe_hdr_rec_t, one coalesced 16-byte store per lane) and the frames are only read; otherwise
 // frames are rewritten in place (bytes 0..31 of each forwarded frame).
-// kLean (linear scan only): the launch has no flow_hash output, no length side array and every
-// non-empty neighbour index staged in LDS, so those paths are not compiled in (fewer live kernel
+// kLean: the launch has no flow_hash output, every non-empty neighbour index staged in LDS and
+// (linear scan) no length side array, so those paths are not compiled in (fewer live kernel
 // arguments: config B/C emit kernels spill 70 SGPRs instead of 96, ~1 % faster).
 template <bool kTssMode, bool kEmit, bool kLean = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
@@ -1413,7 +1413,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
         if (live) a.verdict[i] = code | flags | rbits;
-        if (!kLean && a.lens16 && live) a.lens16[i] = (uint16_t)len;   // 2 B/packet for upe_rule_hist
+        // 2 B/packet for upe_rule_hist (lean linear-scan launches never have the array; the
+        // tuple-space tables it serves always do)
+        if ((kTssMode || !kLean) && a.lens16 && live) a.lens16[i] = (uint16_t)len;
         if (!kLean && a.flow_hash && live) {
             // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
             // key parse_flow_key gives the RX thread (src/rx_pcap.c:71-72), 0 if it fails
@@ -2037,12 +2039,10 @@ int check_lookback(upe_gpu_ctx* c) {
     return 0;
 }
 
-// Kernel variants: bit 1 tuple space, bit 0 emit; kVarLean / kVarLeanInPlace the lean
-// linear-scan kernels.
-constexpr int kVarLean = 4, kVarLeanInPlace = 5;
+// Kernel variants: bit 1 tuple space, bit 0 emit, bit 2 lean.
+constexpr int kVarLean = 4;
 int classify_var(bool tss, bool emit, bool lean) {
-    if (lean && !tss) return emit ? kVarLean : kVarLeanInPlace;
-    return (tss ? 2 : 0) | (emit ? 1 : 0);
+    return (lean ? kVarLean : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
 }
 
 void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
@@ -2064,16 +2064,26 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, false, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, true, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, false, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
     }
     switch (var) {
     case 3: hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
     case 2: hipLaunchKernelGGL((upe_classify<true, false>), dim3(grid), dim3(kBlock), lds, s, a); break;
     case 1: hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case kVarLean:
+    case kVarLean | 1:
         hipLaunchKernelGGL((upe_classify<false, true, true>), dim3(grid), dim3(kBlock), lds, s, a);
         break;
-    case kVarLeanInPlace:
+    case kVarLean:
         hipLaunchKernelGGL((upe_classify<false, false, true>), dim3(grid), dim3(kBlock), lds, s, a);
+        break;
+    case kVarLean | 3:
+        hipLaunchKernelGGL((upe_classify<true, true, true>), dim3(grid), dim3(kBlock), lds, s, a);
+        break;
+    case kVarLean | 2:
+        hipLaunchKernelGGL((upe_classify<true, false, true>), dim3(grid), dim3(kBlock), lds, s, a);
         break;
     default: hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
     }
@@ -2091,11 +2101,17 @@ uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
     case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, true>, kBlock, lds); break;
     case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, false>, kBlock, lds); break;
     case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true>, kBlock, lds); break;
-    case kVarLean:
+    case kVarLean | 1:
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true, true>, kBlock, lds);
         break;
-    case kVarLeanInPlace:
+    case kVarLean:
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false, true>, kBlock, lds);
+        break;
+    case kVarLean | 3:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, true, true>, kBlock, lds);
+        break;
+    case kVarLean | 2:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, false, true>, kBlock, lds);
         break;
     default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false>, kBlock, lds);
     }
@@ -2791,8 +2807,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     }
     // the lean emit kernel when nothing it leaves out is needed (non-empty neighbour indexes
     // all in LDS, no flow_hash, no length side array)
-    const bool lean = !d_flow_hash && !a.lens16 && (arp_slots == 0 || a.arp_lds != 0) &&
-                      (ndp_slots == 0 || a.ndp_lds != 0);
+    const bool lean = !d_flow_hash && (c->tss || !a.lens16) &&
+                      (arp_slots == 0 || a.arp_lds != 0) && (ndp_slots == 0 || a.ndp_lds != 0);
     const int var = classify_var(c->tss, emit, lean);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, var, lds, s);
