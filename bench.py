@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-EVENT_EVERY = 20  # open a kernel-timing sample on every 20th timed step (10 samples at K=200)
+EVENT_EVERY = 20  # a kernel-timing sample on timed steps 10, 30, 50, ... (10 samples at K=200)
 EVENT_SPAN = 5    # each sample's HIP event pair brackets 5 consecutive launches
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
 WORKLOADS = {
@@ -396,7 +396,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
 
     # Kernel timing events ride along in the timed region: a sample opens on every
-    # EVENT_EVERY-th step and its event pair brackets EVENT_SPAN consecutive launches.  Each
+    # EVENT_EVERY-th step (from step EVENT_EVERY / 2: the first launch starts from an idle queue)
+    # and its event pair brackets EVENT_SPAN consecutive launches.  Each
     # event is a queue packet of its own (a few us of latency), so an event pair around every
     # launch would both tax the throughput being measured and inflate the per-launch time; over
     # 5 launches the pair's latency is spread thin (the gaps between those launches remain in
