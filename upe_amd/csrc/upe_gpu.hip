@@ -294,6 +294,8 @@ struct Args {
     uint32_t lb_tag;                 // this launch's flag tag
     uint32_t tw;                     // chunks per tile (kWaves; fewer for small batches)
     uint32_t ntiles;                 // tiles of tw chunks
+    unsigned long long* agree_out;   // host-mapped: (launch + 1) << 2 | start-state agreement bits
+    unsigned long long launch_tag;   // this launch's index + 1
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
@@ -993,7 +995,11 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kLean: the launch has no flow_hash output, every non-empty neighbour index staged in LDS and
 // (linear scan) no length side array, so those paths are not compiled in (fewer live kernel
 // arguments: config B/C emit kernels spill 70 SGPRs instead of 96, ~1 % faster).
-template <bool kTssMode, bool kEmit, bool kLean = false>
+// kNoLB (lean only): chosen once the host has seen a launch start from L1 entries that agree with
+// the tables (agreement then holds until the host changes the tables or the L1 state) or whose
+// family's index is empty; the look-back is not compiled in, and an entry that disagrees with an
+// empty index answers its candidates itself (no packet can hit that table first).
+template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1354,7 +1360,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
             if (cand) flags |= UPE_VF_L1_INIT;
         }
-        if (look4 || look6) {
+        if (kNoLB) {
+            // a disagreeing entry here belongs to a family whose index is empty
+            if (cand && (r.v6 ? look6 : look4)) {
+                hit = true;
+                mlo = r.v6 ? L1[7] : L1[1];
+                mhi = r.v6 ? L1[8] : L1[2];
+            }
+        } else if (look4 || look6) {
             // The starting entry disagrees with the table: publish this chunk's miss-then-hit
             // packets, and give the packets aimed at the entry the entry's MAC unless an earlier
             // packet of their family missed it and hit the table (lookback).
@@ -1538,6 +1551,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
         o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
         o[3] = make_uint4(0u, 0u, 0u, 0u);
+        // tell the host whether this batch started from agreeing entries (upe_gpu_process picks
+        // the kernel without look-back once one has)
+        if (!kNoLB && a.agree_out)
+            __hip_atomic_store(a.agree_out,
+                               a.launch_tag << 2 | (L1[9] ? 1ull : 0ull) | (L1[10] ? 2ull : 0ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     STAMP(5);
 }
@@ -1881,6 +1900,12 @@ struct upe_gpu_ctx {
         uint64_t lo = 0, wb = 0;   // host byte range the slot's copy-back writes
     };
     HostSlot hs[3];
+    // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
+    // device into host-mapped memory, and the first launch whose report counts
+    unsigned long long* agree_h = nullptr;
+    unsigned long long* agree_d = nullptr;
+    uint64_t lb_reset_k = 0;
+    bool no_lb = false;
 };
 
 namespace {
@@ -1993,6 +2018,8 @@ TilePay* pay_slot(upe_gpu_ctx* c, uint64_t k) { return c->pay + (size_t)(k % 2) 
 // Does the L1 state the next batch starts from agree with the tables?  (After l1_sync.)
 int refresh(upe_gpu_ctx* c) {
     if (order_on(c, c->stream) != 0) return -1;
+    c->no_lb = false;   // the entries may disagree with the new tables until a launch says not
+    c->lb_reset_k = c->k;
     hipLaunchKernelGGL(upe_refresh, dim3(1), dim3(64), 0, c->stream, l1_slot(c, c->k),
                        arp_index(c), ndp_index(c));
     HIP_TRY(hipGetLastError());
@@ -2021,6 +2048,8 @@ int arm_state(upe_gpu_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->k = 0;
     c->last_n = 0;
+    c->no_lb = false;
+    c->lb_reset_k = 0;
     return 0;
 }
 
@@ -2039,10 +2068,23 @@ int check_lookback(upe_gpu_ctx* c) {
     return 0;
 }
 
-// Kernel variants: bit 1 tuple space, bit 0 emit, bit 2 lean.
-constexpr int kVarLean = 4;
-int classify_var(bool tss, bool emit, bool lean) {
-    return (lean ? kVarLean : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+// Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only).
+constexpr int kVarCount = 16;
+int classify_var(bool tss, bool emit, bool lean, bool nolb) {
+    return (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+}
+template <int V>
+const void* classify_fn_of() {
+    return reinterpret_cast<const void*>(
+        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0>);
+}
+const void* classify_fn(int var) {
+    static const void* const fns[kVarCount] = {
+        classify_fn_of<0>(), classify_fn_of<1>(), classify_fn_of<2>(), classify_fn_of<3>(),
+        classify_fn_of<4>(), classify_fn_of<5>(), classify_fn_of<6>(), classify_fn_of<7>(),
+        nullptr, nullptr, nullptr, nullptr,
+        classify_fn_of<12>(), classify_fn_of<13>(), classify_fn_of<14>(), classify_fn_of<15>()};
+    return var >= 0 && var < kVarCount ? fns[var] : nullptr;
 }
 
 void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
@@ -2051,42 +2093,14 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
     int dev = 0;
     (void)hipGetDevice(&dev);
     const uint64_t bit = 1ull << (dev & 63);
-    if (!(lds_attr.fetch_or(bit) & bit)) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, true, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<false, false, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, true, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_classify<true, false, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsDynMax);
-    }
-    switch (var) {
-    case 3: hipLaunchKernelGGL((upe_classify<true, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((upe_classify<true, false>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 1: hipLaunchKernelGGL((upe_classify<false, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case kVarLean | 1:
-        hipLaunchKernelGGL((upe_classify<false, true, true>), dim3(grid), dim3(kBlock), lds, s, a);
-        break;
-    case kVarLean:
-        hipLaunchKernelGGL((upe_classify<false, false, true>), dim3(grid), dim3(kBlock), lds, s, a);
-        break;
-    case kVarLean | 3:
-        hipLaunchKernelGGL((upe_classify<true, true, true>), dim3(grid), dim3(kBlock), lds, s, a);
-        break;
-    case kVarLean | 2:
-        hipLaunchKernelGGL((upe_classify<true, false, true>), dim3(grid), dim3(kBlock), lds, s, a);
-        break;
-    default: hipLaunchKernelGGL((upe_classify<false, false>), dim3(grid), dim3(kBlock), lds, s, a);
-    }
+    if (!(lds_attr.fetch_or(bit) & bit))
+        for (int v = 0; v < kVarCount; ++v)
+            if (classify_fn(v))
+                (void)hipFuncSetAttribute(classify_fn(v), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)kLdsDynMax);
+    Args arg = a;
+    void* args[] = {&arg};
+    (void)hipLaunchKernel(classify_fn(var), dim3(grid), dim3(kBlock), args, lds, s);
 }
 
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
@@ -2097,24 +2111,7 @@ uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
     if (it != c->resident.end()) return it->second;
     int per_cu = 0;
     hipError_t e;
-    switch (var) {
-    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, true>, kBlock, lds); break;
-    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, false>, kBlock, lds); break;
-    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true>, kBlock, lds); break;
-    case kVarLean | 1:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, true, true>, kBlock, lds);
-        break;
-    case kVarLean:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false, true>, kBlock, lds);
-        break;
-    case kVarLean | 3:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, true, true>, kBlock, lds);
-        break;
-    case kVarLean | 2:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<true, false, true>, kBlock, lds);
-        break;
-    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upe_classify<false, false>, kBlock, lds);
-    }
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, classify_fn(var), kBlock, lds);
     if (e != hipSuccess) {
         fail(std::string("hipOccupancyMaxActiveBlocksPerMultiprocessor: ") + hipGetErrorString(e));
         return 0;
@@ -2210,6 +2207,20 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
         return bad(e, "hipMalloc payloads");
     if ((e = hipMemset(c->pay, 0, 2 * (size_t)c->paycap * sizeof(TilePay))) != hipSuccess)
         return bad(e, "hipMemset");
+    // host-mapped report of each launch's start-state agreement (the kernel without look-back
+    // is used once one arrives; without it, every launch keeps the look-back)
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->agree_h), sizeof(unsigned long long),
+                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+        *c->agree_h = 0;
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->agree_d), c->agree_h, 0) !=
+            hipSuccess) {
+            (void)hipHostFree(c->agree_h);
+            c->agree_h = nullptr;
+            c->agree_d = nullptr;
+        }
+    } else {
+        c->agree_h = nullptr;
+    }
     if (arm_state(c) != 0) {
         std::string m = g_err;
         upe_gpu_close(c);
@@ -2258,6 +2269,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (c->s_in) (void)hipStreamSynchronize(c->s_in), (void)hipStreamDestroy(c->s_in);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out), (void)hipStreamDestroy(c->s_out);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->agree_h) (void)hipHostFree(c->agree_h);
     delete c;
 }
 
@@ -2809,7 +2821,18 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // all in LDS, no flow_hash, no length side array)
     const bool lean = !d_flow_hash && (c->tss || !a.lens16) &&
                       (arp_slots == 0 || a.arp_lds != 0) && (ndp_slots == 0 || a.ndp_lds != 0);
-    const int var = classify_var(c->tss, emit, lean);
+    // once a launch has been seen starting from agreeing L1 entries (or from an entry whose
+    // family's index is empty), every later one does until the host changes tables or entries
+    if (!c->no_lb && c->agree_h) {
+        const unsigned long long v = __atomic_load_n(c->agree_h, __ATOMIC_ACQUIRE);
+        const unsigned long long tag = v >> 2;
+        if (tag != 0 && tag - 1 >= c->lb_reset_k && ((v & 1) || c->arp_bits == 0) &&
+            ((v & 2) || c->ndp_bits == 0))
+            c->no_lb = true;
+    }
+    a.agree_out = c->no_lb ? nullptr : c->agree_d;
+    a.launch_tag = c->k + 1;
+    const int var = classify_var(c->tss, emit, lean, c->no_lb);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
