@@ -2836,6 +2836,10 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     const uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
+    // the census of the no-look-back counterpart now as well, so that the switch to it (a few
+    // launches later) does not put a synchronous census launch in the middle of a batch stream
+    if (lean && !c->no_lb && resident_grid(c, classify_var(c->tss, emit, true, true), lds, s) == 0)
+        return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
     // more CUs (a 10k-packet batch on ten CUs, four waves per SIMD, took 9.2 us; spread, 7.9).
