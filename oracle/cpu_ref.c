@@ -9,7 +9,7 @@
  *   (1) golden vectors produced by the reference worker itself (oracle/ref_harness.c, which
  *       #includes /root/reference/src/worker.c) — tests/golden/ fixtures, and
  *   (2) the known-answer tests of reference tests/test_suite.c:132-242, 245-299, 332-362,
- *       365-437, 523-590 (restated in tests/test_oracle_kat.py).
+ *       365-437, 523-590 (restated in tests/test_oracle.py).
  *
  * It processes packets strictly one after another, with the worker's one-entry L1 neighbour
  * caches updated sequentially (reference src/worker.c:186-195, 218-225) — deliberately NOT the
@@ -279,7 +279,8 @@ static int control_packet(const upe_ref_env_t *env, uint8_t *d, size_t len, uint
                 size_t off = 78;
                 while (off + 2 <= len) {
                     uint8_t ot = d[off];
-                    size_t ol = (size_t)d[off + 1] * 8;
+                    /* uint8_t, as reference src/worker.c:73: the length wraps at 256 (32 -> 0, 33 -> 8) */
+                    size_t ol = (uint8_t)(d[off + 1] * 8);
                     if (ol == 0 || off + ol > len) break;
                     if (type == 135 && ot == 1 && ol >= 8) {
                         upe_ref_ndp_update(env->ndp, env->ndp_cap, d + 22, d + off + 2);

@@ -97,7 +97,7 @@ static void control_writes(worker_t *w, pktbuf_t *b, uint32_t v) {
         const int ns = d[54] == 135;
         for (size_t off = 78; off + 2 <= b->len;) {
             const uint8_t type = d[off];
-            const size_t olen = (size_t)d[off + 1] * 8;
+            const size_t olen = (uint8_t)(d[off + 1] * 8); /* uint8_t, src/worker.c:73 */
             if (olen == 0 || off + olen > b->len) break;
             if (olen >= 8 && ((ns && type == 1) || (!ns && type == 2))) {
                 ndp_update(w->ndpt, ns ? d + 22 : d + 62, d + off + 2);

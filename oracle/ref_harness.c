@@ -368,3 +368,24 @@ double upe_refh_time(const upe_rule_t *rules, size_t nrules, size_t capacity,
     rule_table_destroy(&rt);
     return med;
 }
+
+/* ---- the RX thread's software RSS (reference src/rx_pcap.c:71-77) -------------------------- */
+/* Per packet: the reference's own parse_flow_key() over a zero-filled pktbuf copy of the frame
+ * and, when it succeeds, the reference's flow_hash() (src/parser.c:113-135); 0 when the parse
+ * fails (the RX thread then falls back to round robin).  ok[i] = 1 where the parse succeeded. */
+int upe_refh_flow_hash(const uint8_t *frames, const uint64_t *desc, size_t n, uint32_t *out,
+                       uint8_t *ok) {
+    static uint8_t buf[PKTBUF_DATA_SIZE];
+    for (size_t i = 0; i < n; i++) {
+        size_t off = (size_t)(desc[i] >> 16), len = (size_t)(desc[i] & 0xFFFF);
+        if (len > PKTBUF_DATA_SIZE) return -1;
+        memset(buf, 0, sizeof buf);
+        memcpy(buf, frames + off, len);
+        flow_key_t k;
+        memset(&k, 0, sizeof k);
+        const int rc = parse_flow_key(buf, len, &k);
+        out[i] = rc == 0 ? flow_hash(&k) : 0u;
+        if (ok) ok[i] = rc == 0;
+    }
+    return 0;
+}

@@ -12,7 +12,14 @@ from upe_amd import synth
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 CASES = ("config_a", "config_b_small", "config_c_small", "config_d_small", "edge_zero",
-         "edge_consistent", "edge_inconsistent")
+         "edge_consistent", "edge_inconsistent", "ndp_walk")
+
+
+def flow_hash(name: str):
+    """The reference RX thread's flow_hash per packet of a golden case (0 where parse_flow_key
+    fails) and whether it parsed (tests/golden/flow_hash.npz)."""
+    z = np.load(os.path.join(GOLDEN, "flow_hash.npz"), allow_pickle=False)
+    return z[name], z[name + "__ok"]
 
 
 def load(name: str):

@@ -31,7 +31,7 @@ def control_kind(frame: np.ndarray, ln: int):
         typ = int(b[54])
         off = 78
         while off + 2 <= ln:
-            ot, ol = int(b[off]), int(b[off + 1]) * 8
+            ot, ol = int(b[off]), (int(b[off + 1]) * 8) & 0xFF   # uint8_t opt_len, src/worker.c:73
             if ol == 0 or off + ol > ln:
                 break
             if typ == 135 and ot == 1 and ol >= 8:

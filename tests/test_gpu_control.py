@@ -35,8 +35,12 @@ def _segmented(worker_factory, wl):
     return (frames, verdict, counters, stats, l1), arp, ndp, writes
 
 
-@pytest.mark.parametrize("case", ["edge_zero", "edge_consistent", "edge_inconsistent"])
+@pytest.mark.parametrize("case", ["edge_zero", "edge_consistent", "edge_inconsistent",
+                                  "ndp_walk"])
 def test_edge_goldens_native_segmented(gpu_worker_factory, case):
+    """ndp_walk: NS / NA frames up to 400 bytes whose option walk crosses the uint8_t opt_len
+    wrap of src/worker.c:73 (length bytes 32, 33, 64), each followed by packets to the address
+    it may teach."""
     wl, ref = golden_io.load(case)
     got, arp, ndp, writes = _segmented(gpu_worker_factory, wl)
     _assert_same(got, ref, case, batch_relative=True)
@@ -46,6 +50,12 @@ def test_edge_goldens_native_segmented(gpu_worker_factory, case):
     # every table write the reference made carries the caller's timestamp
     changed = (arp["valid"] != 0) & (wl.arp["mac"] != arp["mac"]).any(axis=1)
     assert np.all(arp["update_at"][changed] == 1234)
+    if case == "ndp_walk":
+        # the wrap decides what is learned: length byte 32 / 64 teaches nothing, 33 the option
+        # 8 bytes on (MAC 0a:..), never the one 264 bytes on (MAC 0b:..)
+        learned = {bytes(e["ip"])[-1]: bytes(e["mac"]) for e in ndp[ndp["valid"] != 0]}
+        assert 0x00 not in learned and 0x02 not in learned and 0x06 not in learned
+        assert learned[0x01][0] == 0x0A and learned[0x04][0] == 0x0A
 
 
 def _rows(wl):

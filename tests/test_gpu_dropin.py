@@ -44,8 +44,9 @@ def _with_control(n, seed):
 
 @pytest.mark.parametrize("make", [lambda: synth.config_b(n=150_000, seed=61),
                                   lambda: synth.config_c(n=150_000, seed=62),
-                                  lambda: _with_control(60_000, 63)],
-                         ids=["B", "C", "C+control"])
+                                  lambda: _with_control(60_000, 63),
+                                  lambda: synth.config_ndp_walk(repeat=20)],
+                         ids=["B", "C", "C+control", "NS/NA opt_len wrap"])
 def test_reference_pipeline_with_gpu_worker(make):
     wl = make()
     lib = _lib()

@@ -1,6 +1,8 @@
 """GPU: software RSS in the classify pass (flow_hash, reference src/parser.c:113-135 as the RX
 thread applies it, src/rx_pcap.c:71-72) and the ordered egress list (the frames process_packet
-queues for tx_send_batch, src/worker.c:240-243), against the oracle."""
+queues for tx_send_batch, src/worker.c:240-243).  Pinned to the reference itself: the hashes to
+the reference's own parse_flow_key + flow_hash per packet (tests/golden/flow_hash.npz, made from
+oracle/_ref), the egress lists to the reference worker's golden verdicts."""
 from __future__ import annotations
 
 import ctypes
@@ -28,8 +30,8 @@ def _expected_hashes(wl):
     return out
 
 
-@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "config_d_small",
-                                  "edge_zero"])
+@pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
+                                  "config_d_small", "edge_zero", "ndp_walk"])
 def test_flow_hash_in_pass(gpu_worker_factory, case):
     wl, ref = golden_io.load(case)
     w = gpu_worker_factory(wl.capacity)
@@ -45,8 +47,11 @@ def test_flow_hash_in_pass(gpu_worker_factory, case):
         b.free()
     finally:
         w.close()
-    assert np.array_equal(got, _expected_hashes(wl))
-    if not case.startswith("edge"):
+    want, parsed = golden_io.flow_hash(case)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} hashes differ from the reference's, first {bad[:8].tolist()}"
+    assert np.array_equal(want, _expected_hashes(wl))   # the restatement agrees too
+    if not case.startswith("edge") and case != "ndp_walk":
         assert np.array_equal(v, ref["verdict"])
 
 
@@ -80,3 +85,40 @@ def test_egress_list_in_order(gpu_worker_factory, n, code):
     want = np.nonzero((v & 0xF) == code)[0]
     assert k == want.size
     assert np.array_equal(got[:k], want.astype(np.uint32))
+
+
+@pytest.mark.parametrize("emit", [False, True])
+@pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
+                                  "config_d_small"])
+def test_egress_list_matches_reference_order(gpu_worker_factory, case, emit):
+    """The FWD list (and the DROP_RULE list) built on the device from the GPU's verdicts equals
+    the order in which the REFERENCE worker queued those packets: the indexes whose golden
+    verdict code is FWD, ascending (src/worker.c:240-243, flushed in order by :287-303)."""
+    wl, ref = golden_io.load(case)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        b = gpu.DeviceBatch(w, wl.frames, wl.desc)
+        b.run_emit() if emit else b.run()
+        got = {}
+        for code in (V_FWD, V_DROP_RULE):
+            index = w.malloc(4 * wl.n)
+            count = w.malloc(8)
+            w.compact(b.verdict, wl.n, code, index, count)
+            k_arr = np.zeros(1, np.uint64)
+            w.d2h(k_arr, count)
+            w.sync()
+            lst = np.zeros(max(int(k_arr[0]), 1), np.uint32)
+            if k_arr[0]:
+                w.d2h(lst, index)
+            w.sync()
+            got[code] = lst[: int(k_arr[0])]
+            w.free(index)
+            w.free(count)
+        b.free()
+    finally:
+        w.close()
+    for code in (V_FWD, V_DROP_RULE):
+        want = np.nonzero((ref["verdict"] & 0xF) == code)[0].astype(np.uint32)
+        assert want.size > 0 or code != V_FWD or case == "config_a"
+        assert np.array_equal(got[code], want), f"code {code}: egress order differs"

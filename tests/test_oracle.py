@@ -243,3 +243,21 @@ def test_restated_vs_reference_fresh_seeds(seed):
         assert a.counters.tobytes() == b.counters.tobytes()
         assert np.array_equal(a.rule_stats, b.rule_stats)
         assert a.l1.tobytes() == b.l1.tobytes()
+
+
+@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "edge_zero", "ndp_walk"])
+def test_restated_flow_hash_matches_reference(case):
+    """The restated parse + flow_hash (oracle/cpu_ref.c) equals the reference's own
+    parse_flow_key + flow_hash per packet (tests/golden/flow_hash.npz, from oracle/_ref) — the
+    value pin that reference tests/test_suite.c:245-299 (symmetry only) does not give."""
+    from upe_amd.layout import desc_lens, desc_offsets
+
+    wl, _ = golden_io.load(case)
+    want, parsed = golden_io.flow_hash(case)
+    lib = oracle.oracle_lib()
+    offs, lens = desc_offsets(wl.desc), desc_lens(wl.desc)
+    for i in range(wl.n):
+        rc, key = oracle.parse(bytes(wl.frames[offs[i]:offs[i] + int(lens[i])]), int(lens[i]))
+        assert (rc == 0) == bool(parsed[i]), i
+        got = lib.upe_ref_flow_hash(_p(key)) if rc == 0 else 0
+        assert got == int(want[i]), i

@@ -3221,7 +3221,8 @@ int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_
             }
             const bool ns = f[54] == 135;
             for (size_t off = 78; off + 2 <= len;) {
-                const uint32_t ot = f[off], ol = (uint32_t)f[off + 1] * 8u;
+                // uint8_t opt_len, as the reference's (src/worker.c:73): 32 wraps to 0, 33 to 8
+                const uint32_t ot = f[off], ol = (uint8_t)(f[off + 1] * 8u);
                 if (ol == 0 || off + ol > len) break;
                 if (ol >= 8 && ((ns && ot == 1) || (!ns && ot == 2))) {
                     if (ndp_capacity) {

@@ -818,3 +818,48 @@ def config_edge(repeat: int = 4, seed: int = 5) -> Workload:
                          (bytes.fromhex("20010db8000000000000000000000002"),
                           bytes.fromhex("bbccddee0002"))])
     return Workload("edge", frames, desc, edge_rules(), 64, arp, ndp)
+
+
+def config_ndp_walk(repeat: int = 3) -> Workload:
+    """Long NS / NA frames (up to 400 bytes) whose option walk crosses the uint8_t width of
+    reference src/worker.c:73 (`uint8_t opt_len = data[off + 1] * 8`): a length byte of 32 or 64
+    wraps to 0 (the walk stops, nothing is learned), 33 wraps to 8 (the walk advances 8 bytes,
+    not 264).  Each control frame is followed by IPv6 packets to the address it teaches, so a
+    wrong walk shows up in the forwarded bytes and in the final NDP table.  Used by the
+    control-packet and drop-in tests."""
+    V6S = bytes.fromhex("20010db8000000000000000000000001")
+    tgt = [bytes.fromhex("20010db80000000000000000000001%02x" % k) for k in range(8)]
+    MA, MB = bytes.fromhex("0a0000000a0a"), bytes.fromhex("0b0000000b0b")
+
+    def opts(first_len: int, typ: int, total: int) -> bytes:
+        # option 0: unknown type 5 with length byte first_len; an SLLA / TLLA (MAC A) 8 bytes
+        # later and another (MAC B) where the un-wrapped length would land
+        o = bytearray(total - 78)
+        o[0], o[1] = 5, first_len
+        o[8:16] = bytes([typ, 1]) + MA
+        far = (first_len * 8) & 0xFFFF
+        if 0 < far and far + 8 <= len(o):
+            o[far:far + 8] = bytes([typ, 1]) + MB
+        return bytes(o)
+
+    frames = []
+    for k, (first, total) in enumerate([(32, 350), (33, 360), (64, 400), (31, 300),
+                                        (33, 290), (1, 120), (32, 250), (0, 200)]):
+        ns = k % 2 == 0
+        ip = tgt[k]
+        if ns:   # NS: learns (ip6.src, SLLA)
+            f = _frame(_eth(0x86DD), _ip6(58, ip, V6S), bytes([135, 0, 0, 0, 0, 0, 0, 0]) + ip,
+                       opts(first, 1, total))
+        else:    # NA: learns (target, TLLA)
+            f = _frame(_eth(0x86DD), _ip6(58, V6S, ip), bytes([136, 0, 0, 0, 0x60, 0, 0, 0]) + ip,
+                       opts(first, 2, total))
+        probe = _frame(_eth(0x86DD), _ip6(17, V6S, ip), _udp(4000 + k, 53))
+        frames += [(probe, len(probe)), (f, len(f)), (probe, len(probe)), (probe, len(probe))]
+    frames = frames * repeat
+    lens = np.array([ln for _, ln in frames], dtype=np.int64)
+    h = np.zeros((len(frames), 512), dtype=np.uint8)
+    for i, (f, _) in enumerate(frames):
+        h[i, :len(f)] = np.frombuffer(f, np.uint8)
+    fr, desc = pack_frames(h, lens)
+    ndp = ndp_table(16, [(tgt[7], bytes.fromhex("0c0000000c0c"))])
+    return Workload("ndp_walk", fr, desc, edge_rules(), 64, arp_table(16, []), ndp)
