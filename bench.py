@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ALLOWED_CPUS = sorted(os.sched_getaffinity(0))   # the process's CPUs, before the host thread is pinned
 EVENT_EVERY = 20  # a kernel-timing sample on timed steps 10, 30, 50, ... (10 samples at K=200)
 EVENT_SPAN = 5    # each sample's HIP event pair brackets 5 consecutive launches
 METRIC = "Mpps parse+classify (device-resident), 64B & IMIX; achieved HBM GB/s vs peak"
@@ -161,14 +162,24 @@ def pmc_traffic(config: str, packets: int, mode: str):
     return d["traffic_bytes_per_launch"] if d.get("packets") == packets else None
 
 
-def cpu_baseline(wl, threads: int) -> dict:
+def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
+    """The reference worker timed on this host: one shard and calloc'd worker_t per thread, each
+    pinned to its own core — the GPU's NUMA-local cores first (`local`), then the rest of the
+    affinity mask.  `threads` is this job's CPU share (16 per GPU on the GPU box; the machine's
+    other cores belong to other jobs), reported with the spread of the passes."""
     import oracle
 
     sample = f"{wl.n} packets of the same workload, median of 9 passes after 1 warm-up"
     if oracle.ref_available():
-        cpus = sorted(os.sched_getaffinity(0))[:threads]
-        v1 = oracle.time_reference(wl, threads=1, cpus=cpus[:1], reps=9)
-        vn = oracle.time_reference(wl, threads=len(cpus), cpus=cpus, reps=9) if len(cpus) > 1 else v1
+        allowed = ALLOWED_CPUS
+        order = [c for c in (local or []) if c in allowed] + \
+            [c for c in allowed if c not in (local or [])]
+        cpus = order[:threads]
+        r1, rn = [], []
+        v1 = oracle.time_reference(wl, threads=1, cpus=cpus[:1], reps=9, rates=r1)
+        vn = (oracle.time_reference(wl, threads=len(cpus), cpus=cpus, reps=9, rates=rn)
+              if len(cpus) > 1 else v1)
+        rn = rn or r1
         try:
             model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                      if l.startswith("model name")][0]
@@ -176,6 +187,10 @@ def cpu_baseline(wl, threads: int) -> dict:
             model = "unknown"
         return {"value": round(vn / 1e6, 3), "unit": "Mpps", "cores": len(cpus),
                 "kind": "reference", "single_core_value": round(v1 / 1e6, 3),
+                "spread": {"min": round(rn[0] / 1e6, 3), "median": round(vn / 1e6, 3),
+                           "max": round(rn[-1] / 1e6, 3), "passes": len(rn),
+                           "single_core_min_max": [round(r1[0] / 1e6, 3), round(r1[-1] / 1e6, 3)]},
+                "cpus": cpus, "cpus_online": os.cpu_count(), "cpus_in_affinity": len(allowed),
                 "cpu_model": model,
                 "sample": sample + "; reference src/worker.c process_packet + TX-flush loop "
                           "(bursts of 32), one shard and calloc'd worker_t per pinned thread"}
@@ -301,13 +316,15 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="B", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=None, help="override batch size")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU baseline threads: this job's CPU share on the GPU box (16 per GPU; "
+                         "the other cores of the machine run other jobs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-copies", type=int, default=1024)
-    ap.add_argument("--host-reps", type=int, default=0,
-                    help="passes of the host round-trip leg (default 0: skip it, so that a "
-                         "rocprof summary of the default command holds only full-batch "
-                         "launches; DESIGN.md quotes a --host-reps 10 run)")
+    ap.add_argument("--host-reps", type=int, default=5,
+                    help="passes of the host round-trip leg (pinned host batch -> H2D -> "
+                         "classify -> D2H), after every timed leg; 0 skips it.  Its launches "
+                         "are a separate leg of a rocprof trace (tools/kernel_legs.py)")
     ap.add_argument("--host-chunk", type=int, default=0)
     ap.add_argument("--workers-per-gpu", type=int, default=0,
                     help="also time W worker contexts sharing this GPU, each on its own stream "
@@ -348,6 +365,17 @@ def main() -> None:
         torch.cuda.set_device(local)
 
     from upe_amd import gpu, shard, synth
+
+    # this rank's host thread on a core of its GPU's NUMA node (its pinned buffers then come from
+    # that node), as the reference pins each worker thread (src/affinity.c:48, src/main.c:143-175)
+    local_cpus, numa_node = [], -1
+    pinned_cpu = None
+    try:
+        local_cpus, numa_node = gpu.local_cpus(local)
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        pinned_cpu = gpu.pin_self(local, local_rank)
+    except (gpu.UpeGpuError, AttributeError) as e:   # AttributeError: an older diagnostic build
+        print(f"bench: no NUMA pinning ({e})", file=sys.stderr)
 
     # this rank's static shard: a full batch of the configuration, its own seed
     make = {"A": synth.config_a, "B": synth.config_b, "C": synth.config_c,
@@ -494,6 +522,8 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded upe_amd.synth, per-rank shard), resident in HBM",
+            "host_thread": {"cpu": pinned_cpu, "numa_node": numa_node,
+                            "gpu_local_cpus": len(local_cpus)},
             "config": {"workload": WORKLOADS[args.config], "packets_per_gpu_step": n,
                        "rules": int(len(wl.rules)), "parallelism": f"static shards x{world}, "
                        "tables replicated, no RCCL on the data path",
@@ -551,7 +581,8 @@ def main() -> None:
             }
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             # config A is the reference's one-worker pcap replay: time it on one core
-            out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads,
+                                               local_cpus)
         print(json.dumps(out), flush=True)
     worker.close()
     if dist:

@@ -180,6 +180,17 @@ const char *upe_gpu_last_error(void);
 /* Number of visible GPUs, or -1. */
 int upe_gpu_device_count(void);
 
+/* Host CPUs local to a GPU (its PCI function's NUMA node, sysfs local_cpulist) that the calling
+ * thread may run on: up to `cap` of them into cpus (may be NULL), *numa_node (may be NULL) = the
+ * node or -1.  Returns how many there are, or -1. */
+int upe_gpu_local_cpus(int device, int *cpus, size_t cap, int *numa_node);
+
+/* Pin the calling thread to the slot-th CPU local to `device` (modulo their number), as the
+ * reference pins each worker thread (affinity_pin_self, src/affinity.c:48; assign_cores,
+ * src/main.c:143-175).  Pinned host buffers allocated afterwards by this thread come from the
+ * GPU's NUMA node.  Returns the CPU, or -1. */
+int upe_gpu_pin_self(int device, int slot);
+
 /* Open a context on `device`, with its own HIP stream.  Replaces the per-worker state set up by
  * worker_init() (reference src/worker.c:309-330): counters, rule_stats sized by
  * rule_capacity (= rt->capacity, src/worker.c:326), calloc'd L1 caches. */
@@ -323,6 +334,20 @@ int upe_gpu_sync(upe_gpu_ctx_t *ctx, void *stream);
 /* Summary of the most recent upe_gpu_process() (synchronises). */
 int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
 
+/* How the most recent classify launch ran (synchronises; diagnostics and tests).  A launch that
+ * starts from an L1 entry disagreeing with its table resolves the packets aimed at that entry by
+ * a bounded look-back; a wave that stops waiting (a workgroup it needs is not resident yet)
+ * defers them, and the launch's last workgroup answers them. */
+typedef struct {
+    uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back */
+    uint32_t grid;     /* workgroups of the launch */
+    uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
+                          workgroup (0 when the look-back was not live) */
+    uint32_t reserved;
+    uint64_t launches; /* classify launches of this context so far */
+} upe_launch_info_t;
+int upe_gpu_launch_info(upe_gpu_ctx_t *ctx, upe_launch_info_t *info);
+
 /* Accumulated worker counters and rule_stats[0..capacity) (synchronises). */
 int upe_gpu_get_stats(upe_gpu_ctx_t *ctx, upe_counters_t *counters, upe_rule_stat_t *rule_stats,
                       size_t capacity);
@@ -402,5 +427,6 @@ UPE_STATIC_ASSERT(sizeof(upe_ndp_entry_t) == 40, "ndp_entry_t layout");
 UPE_STATIC_ASSERT(offsetof(upe_ndp_entry_t, valid) == 32, "ndp_entry_t.valid");
 UPE_STATIC_ASSERT(sizeof(upe_rule_stat_t) == 16, "rule_stat_t layout");
 UPE_STATIC_ASSERT(sizeof(upe_hdr_rec_t) == 16, "upe_hdr_rec_t layout");
+UPE_STATIC_ASSERT(sizeof(upe_launch_info_t) == 24, "upe_launch_info_t layout");
 
 #endif /* UPE_GPU_H */

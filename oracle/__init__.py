@@ -85,7 +85,7 @@ def ref_lib() -> ctypes.CDLL:
                                          ctypes.c_uint32, _P, _P, _P, _SZ, _P, _P, _P]
         lib.upe_refh_time.restype = ctypes.c_double
         lib.upe_refh_time.argtypes = [_P, _SZ, _SZ, _P, _SZ, _P, _SZ, _P, ctypes.c_uint32, _P, _P,
-                                      _SZ, ctypes.c_int, _P, ctypes.c_int]
+                                      _SZ, ctypes.c_int, _P, ctypes.c_int, _P]
         _ref = lib
     return _ref
 
@@ -154,15 +154,20 @@ def run_reference(wl, presorted: bool = False, l1=None) -> Result:
     return Result(frames, verdict, cnt, st, l1, arp, ndp, sorted_out)
 
 
-def time_reference(wl, threads: int = 1, cpus=None, reps: int = 5) -> float:
-    """Median packets/s of the reference worker over the workload (see upe_refh_time)."""
+def time_reference(wl, threads: int = 1, cpus=None, reps: int = 5, rates=None) -> float:
+    """Median packets/s of the reference worker over the workload (see upe_refh_time); `rates`
+    (a list) receives every rep's rate, ascending."""
     lib = ref_lib()
+    out = np.zeros(reps, np.float64)
     rs = np.ascontiguousarray(wl.rules_sorted, dtype=RULE_DTYPE)
     eth = _eth(wl)
     cpu_arr = None if cpus is None else np.ascontiguousarray(np.asarray(cpus, dtype=np.int32))
-    return lib.upe_refh_time(_ptr(rs), len(rs), wl.capacity, _ptr(wl.arp), len(wl.arp),
+    med = lib.upe_refh_time(_ptr(rs), len(rs), wl.capacity, _ptr(wl.arp), len(wl.arp),
                              _ptr(wl.ndp), len(wl.ndp), _ptr(eth), wl.ip4_addr, _ptr(wl.frames),
-                             _ptr(wl.desc), wl.n, threads, _ptr(cpu_arr), reps)
+                             _ptr(wl.desc), wl.n, threads, _ptr(cpu_arr), reps, _ptr(out))
+    if rates is not None:
+        rates.extend(float(x) for x in out)
+    return med
 
 
 def parse(frame: bytes, length: int | None = None):

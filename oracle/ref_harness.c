@@ -316,13 +316,14 @@ static void *shard_main(void *arg) {
  * Time the reference worker over a batch: `threads` workers, each pinned to cpus[t] (or
  * unpinned when cpus is NULL), one contiguous shard each, own calloc'd worker_t, shared rule
  * table and neighbour tables (as src/main.c:444-456).  rules are final sorted rt->rules.
- * Returns the median over `reps` of (n / max-over-threads seconds) in packets/s, or -1.
+ * Returns the median over `reps` of (n / max-over-threads seconds) in packets/s, or -1;
+ * rates_out (optional, `reps` doubles) receives every rep's rate, ascending.
  */
 double upe_refh_time(const upe_rule_t *rules, size_t nrules, size_t capacity,
                      const upe_arp_entry_t *arp, size_t arp_cap, const upe_ndp_entry_t *ndp,
                      size_t ndp_cap, const uint8_t eth_addr[6], uint32_t ip4_addr,
                      const uint8_t *frames, const uint64_t *desc, size_t n, int threads,
-                     const int *cpus, int reps) {
+                     const int *cpus, int reps, double *rates_out) {
     if (threads < 1 || reps < 1 || n == 0) return -1;
     rule_table_t rt;
     if (build_rules(&rt, rules, nrules, capacity, 1) != 0) return -1;
@@ -361,6 +362,7 @@ double upe_refh_time(const upe_rule_t *rules, size_t nrules, size_t capacity,
             double x = rate[j]; rate[j] = rate[j - 1]; rate[j - 1] = x;
         }
     double med = rate[reps / 2];
+    if (rates_out) memcpy(rates_out, rate, (size_t)reps * sizeof(double));
     free(rate); free(secs); free(th); free(sh);
     pthread_barrier_destroy(&bar);
     arp_table_destroy(&arpt);

@@ -60,6 +60,7 @@ int main(void) {
   P(upe_l1_state_t, last_ndp_mac);
   S(upe_counters_t); S(upe_batch_info_t); P(upe_batch_info_t, n_ctrl); P(upe_batch_info_t, first_ctrl);
   S(upe_rule_stat_t);
+  S(upe_launch_info_t); P(upe_launch_info_t, deferred); P(upe_launch_info_t, launches);
   return 0;
 }
 """
@@ -93,6 +94,10 @@ def test_struct_layouts_match_numpy_mirrors():
     assert got["upe_batch_info_t"] == layout.BATCH_INFO_DTYPE.itemsize
     assert got["upe_batch_info_t.n_ctrl"] == layout.BATCH_INFO_DTYPE.fields["n_ctrl"][1]
     assert got["upe_rule_stat_t"] == layout.RULE_STAT_DTYPE.itemsize
+    LI = layout.LAUNCH_INFO_DTYPE
+    assert got["upe_launch_info_t"] == LI.itemsize
+    assert got["upe_launch_info_t.deferred"] == LI.fields["deferred"][1]
+    assert got["upe_launch_info_t.launches"] == LI.fields["launches"][1]
 
 
 def test_header_compiles_as_c_and_cpp():

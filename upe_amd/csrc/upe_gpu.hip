@@ -52,6 +52,9 @@
 // the entry and hit the table: each 64-packet chunk publishes whether it holds such a packet,
 // and a chunk with candidates looks back over the chunks before it (decoupled look-back).
 #include <hip/hip_runtime.h>
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -120,6 +123,9 @@ constexpr int kReps = 32;              // replicas of the per-batch accumulators
 // 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 256 no fold of the
 // previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
+#ifndef UPE_DIAG_NO_DONE
+#define UPE_DIAG_NO_DONE 0   // diagnostic timing builds only: no deferred-candidate repair
+#endif
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
 // rv4[i]: header + first address word, used for every packet:
@@ -176,7 +182,11 @@ struct __attribute__((aligned(128))) BatchAcc {
     uint32_t ctrl[kReps];                  // kNone - first control packet (max)
     uint32_t grid;                         // the batch's grid
     uint32_t n;                            // the batch's size
-    uint32_t pad[30];
+    // look-back give-ups (a launch that started from a disagreeing L1 entry): workgroups that have
+    // finished, deferred (chunk, family) entries, and "some wave gave up" (later waves then wait
+    // for no unpublished flag at all)
+    uint32_t done, ndefer, giveup;
+    uint32_t pad[27];
 };
 // Payload of a workgroup's last table hit per family; the next batch reads the one the batch
 // maximum points at.
@@ -199,8 +209,7 @@ struct DevState {
     DevL1 l1[2];
     BatchAcc acc[3];
     unsigned long long totals[8];                           // cumulative, upe_counters_t order
-    uint32_t lb_timeout;                                    // a look-back gave up (grid not resident)
-    uint32_t pad0[15];
+    uint32_t pad0[16];
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
     uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
@@ -296,6 +305,8 @@ struct Args {
     uint32_t ntiles;                 // tiles of tw chunks
     unsigned long long* agree_out;   // host-mapped: (launch + 1) << 2 | start-state agreement bits
     unsigned long long launch_tag;   // this launch's index + 1
+    uint32_t* defer;                 // deferred look-back candidates: index | family << 31
+    uint32_t lb_spin;                // longest look-back wait, 100 MHz ticks (then defer)
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
@@ -915,14 +926,18 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
 // (a wave's 64 packets of a tile) publishes whether it holds such a packet; a wave holding
 // candidates reads the flags of the chunks before it, nearest first, until one holds such a
 // packet or one already knows the answer for everything up to it (LB_KNOWN*), waiting for any
-// chunk that has not published yet.  Chunks only ever wait for lower chunks, and every chunk
-// of the grid is resident (census), so the wait ends; a give-up after ~20 ms (which a resident
-// grid never reaches) is reported through DevState::lb_timeout.  Returns, for the families in
-// `need` (bit 0 v4, bit 1 v6), whether an earlier chunk holds a miss-then-hit packet.
+// chunk that has not published yet — but only for `spin` ticks of the 100 MHz clock.  The wait
+// must be bounded: a chunk it waits for may belong to a workgroup that is not resident (another
+// kernel holds CUs, or another context's grid on the same GPU) and can only start once a
+// resident one exits.  A wave that gives up defers its candidates (upe_classify: they keep the
+// table's answer for now, and the launch's last workgroup repairs them once every chunk has
+// published), so no workgroup ever waits on one that has not started.  Returns the families of
+// `need` (bit 0 v4, bit 1 v6) still unresolved (0 = all resolved); `got` = for the resolved
+// ones, whether an earlier chunk holds a miss-then-hit packet.
 // ------------------------------------------------------------------------------------------
-__device__ uint32_t lookback(uint32_t* lb, uint32_t chunk, uint32_t tag, uint32_t need, int lane,
-                             uint32_t* timeout) {
-    uint32_t got = 0;
+__device__ uint32_t lookback(const uint32_t* lb, uint32_t chunk, uint32_t tag, uint32_t need,
+                             int lane, uint32_t spin, uint32_t& got) {
+    got = 0;
     int64_t base = chunk;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
     while (need && base > 0) {
@@ -935,11 +950,7 @@ __device__ uint32_t lookback(uint32_t* lb, uint32_t chunk, uint32_t tag, uint32_
                 ready = (f >> 6) == tag;
             }
             if (__all(ready)) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000u) {
-                if (lane == 0)
-                    __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return got;
-            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 >= spin) return need;   // defer
             __builtin_amdgcn_s_sleep(2);
         }
 #pragma unroll
@@ -957,7 +968,78 @@ __device__ uint32_t lookback(uint32_t* lb, uint32_t chunk, uint32_t tag, uint32_
         }
         base -= 64;
     }
-    return got;
+    return 0;   // walked to chunk 0: what is still needed has no earlier miss-then-hit packet
+}
+
+// The launch's last workgroup (wave 0) answers the candidates that waves deferred: every chunk
+// has been processed by now, so every flag word of this launch is written or about to land.  F4 /
+// F6 = the first chunk holding a miss-then-hit packet of each family; a deferred candidate of
+// chunk c takes the starting entry's MAC iff F >= c (the earlier lanes of its own chunk were
+// checked when it deferred).  entries[e] = packet index | family << 31 (1 = IPv6).
+#ifndef UPE_REPAIR_UNROLL
+#define UPE_REPAIR_UNROLL 4
+#endif
+constexpr int kRepairUnroll = UPE_REPAIR_UNROLL;
+struct Repair {
+    uint32_t mac4_lo, mac4_hi, mac6_lo, mac6_hi;   // the batch's starting L1 entries' MACs
+};
+template <bool kEmit>
+__device__ void repair_deferred(const Args& a, uint32_t nd, int lane, Repair m) {
+    const uint32_t nchunks = (a.n + 63u) / 64u;
+    uint32_t last = 0;   // the highest chunk with a deferred candidate: F beyond it does not matter
+    for (uint32_t e = lane; e < nd; e += 64) last = max(last, (a.defer[e] & 0x7FFFFFFFu) / 64u);
+    last = wave_reduce<2>(last);
+    uint32_t F4 = kNone, F6 = kNone;
+    for (uint32_t b = 0; b <= last && b < nchunks && (F4 == kNone || F6 == kNone); b += 64) {
+        const uint32_t j = b + (uint32_t)lane;
+        uint32_t f = 0;
+        if (j < nchunks && j <= last) {
+            do {
+                f = __hip_atomic_load(&a.lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((f >> 6) != a.lb_tag);
+        }
+        const unsigned long long b4 = __ballot(f & LB_FP4), b6 = __ballot(f & LB_FP6);
+        if (F4 == kNone && b4) F4 = b + (uint32_t)__builtin_ctzll(b4);
+        if (F6 == kNone && b6) F6 = b + (uint32_t)__builtin_ctzll(b6);
+    }
+    const uint32_t w1_4 = m.mac4_hi | (a.port_mac_lo << 16), w1_6 = m.mac6_hi | (a.port_mac_lo << 16);
+    const uint32_t w2 = (a.port_mac_lo >> 16) | (a.port_mac_hi << 16);
+    // kRepairUnroll entries per lane at a time, their loads issued together (one wave does this)
+    constexpr int U = kRepairUnroll;
+    for (uint32_t e0 = 0; e0 < nd; e0 += U * 64) {
+        uint32_t x[U], v[U];
+        uint4 q[U];
+        bool p[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t e = e0 + 64u * k + (uint32_t)lane;
+            x[k] = e < nd ? a.defer[e] : kNone;
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t i = x[k] & 0x7FFFFFFFu;
+            const bool v6 = (x[k] >> 31) != 0;
+            // an earlier chunk's packet took the table: the provisional answer stands
+            p[k] = x[k] != kNone && (v6 ? F6 : F4) >= i / 64u;
+            if (p[k]) {
+                v[k] = a.verdict[i];
+                q[k] = kEmit ? a.hdr[i]
+                             : *reinterpret_cast<const uint4*>(a.frames + ((size_t)(a.desc[i] >> 20) << 4));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (!p[k]) continue;
+            const uint32_t i = x[k] & 0x7FFFFFFFu;
+            const bool v6 = (x[k] >> 31) != 0;
+            a.verdict[i] = v[k] | UPE_VF_NEIGH_HIT;
+            const uint4 o = make_uint4(v6 ? m.mac6_lo : m.mac4_lo, v6 ? w1_6 : w1_4, w2, q[k].w);
+            if (kEmit)
+                a.hdr[i] = o;
+            else
+                *reinterpret_cast<uint4*>(a.frames + ((size_t)(a.desc[i] >> 20) << 4)) = o;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1147,6 +1229,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
             for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0ull;
             if (lane < kReps) acc_next(a)->ctrl[lane] = 0u;
+            if (lane < 3) (&acc_next(a)->done)[lane] = 0u;   // done, ndefer, giveup
         }
     };
     auto fold_start = [&]() {
@@ -1341,6 +1424,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         bool hit = false;      // the packet gets a MAC: the table's (or the starting entry's)
         bool cand = false;     // destination == starting L1 entry (ARP: and != 0)
         bool wrote1 = false;
+        bool deferred = false;   // this wave deferred candidates (wave-uniform)
         if (code == UPE_V_FWD) {
             if (r.ttl <= 1u) {                         // src/worker.c:165-172, 204-211
                 code = UPE_V_DROP_TTL;
@@ -1382,25 +1466,48 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const uint32_t need = (__ballot(c4) ? (uint32_t)LB_FP4 : 0u) |
                                   (__ballot(c6) ? (uint32_t)LB_FP6 : 0u);
             if (need) {
-                const uint32_t before = lookback(a.lb, chunk, a.lb_tag, need, lane,
-                                                 &a.st->lb_timeout);
+                // once any wave of the launch has given up, wait for no unpublished flag at all
+                const uint32_t spin = __hip_atomic_load(&acc_cur(a)->giveup, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) ? 0u : a.lb_spin;
+                uint32_t before = 0;
+                const uint32_t left = lookback(a.lb, chunk, a.lb_tag, need, lane, spin, before);
                 const unsigned long long lt = (1ull << lane) - 1ull;
                 const bool prior4 = (before & LB_FP4) || (b4 & lt);
                 const bool prior6 = (before & LB_FP6) || (b6 & lt);
-                if ((c4 && !prior4) || (c6 && !prior6)) {
+                const bool r4 = c4 && !(left & LB_FP4), r6 = c6 && !(left & LB_FP6);
+                if ((r4 && !prior4) || (r6 && !prior6)) {
                     hit = true;
                     mlo = r.v6 ? L1[7] : L1[1];
                     mhi = r.v6 ? L1[8] : L1[2];
                 }
-                // what this chunk now knows about everything up to it
+                // what this chunk now knows about everything up to it (resolved families only)
+                const uint32_t res = need & ~left;
                 uint32_t kn = 0;
-                if (need & LB_FP4)
+                if (res & LB_FP4)
                     kn |= LB_KNOWN4 | (((before & LB_FP4) || b4) ? (uint32_t)LB_INCL4 : 0u);
-                if (need & LB_FP6)
+                if (res & LB_FP6)
                     kn |= LB_KNOWN6 | (((before & LB_FP6) || b6) ? (uint32_t)LB_INCL6 : 0u);
-                if (lane == 0)
+                if (lane == 0 && kn)
                     __hip_atomic_store(&a.lb[chunk], tag | fpb | kn, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                if (left) {
+                    // Gave up: the candidates an earlier packet of this chunk does not answer keep
+                    // the table's answer for now and list themselves (index | family << 31); the
+                    // launch's last workgroup repairs them (repair_deferred) once every chunk has
+                    // published.
+                    const bool dl = (c4 && (left & LB_FP4) && !(b4 & lt)) ||
+                                    (c6 && (left & LB_FP6) && !(b6 & lt));
+                    const unsigned long long dm = __ballot(dl);
+                    uint32_t base = 0;
+                    if (lane == 0) {
+                        __hip_atomic_store(&acc_cur(a)->giveup, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        if (dm) base = atomicAdd(&acc_cur(a)->ndefer, (uint32_t)__popcll(dm));
+                    }
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    if (dl) a.defer[base + (uint32_t)__popcll(dm & lt)] = i | (r.v6 ? 0x80000000u : 0u);
+                    deferred = dm != 0;
+                }
             }
         }
         if (hit) flags |= UPE_VF_NEIGH_HIT;
@@ -1437,6 +1544,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                       : (r.s[0] ^ r.d[0]);
             a.flow_hash[i] = ok ? h : 0u;
         }
+        // a deferring wave's outputs and entries are complete before its workgroup counts itself
+        // done (the repair reads and patches them)
+        if (!kNoLB && deferred) __threadfence();
 
         // ---- rule_stats: LDS histogram (same-address lanes serialise in the LDS atomic unit,
         // cheaper than a cross-lane reduction per distinct rule).  One 64-bit atomic per packet:
@@ -1495,12 +1605,36 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     STAMP(10);
 
+    // A look-back-live launch counts its finished workgroups; the last one answers whatever the
+    // waves deferred (nobody waits for that: a workgroup that is not resident yet delays only the
+    // count).  Wave 1 counts, with one atomic whose return it waits for, issued before anything
+    // else it has to send, while wave 0 flushes the accumulators and the other waves the
+    // mid-size rule_stats, so the round trip overlaps those.
+    constexpr int kCounter = kWaves > 1 ? 1 : 0;
+    const bool counting = !kNoLB && !UPE_DIAG_NO_DONE && (look4 || look6);
+    if (counting && wave == kCounter) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&acc_cur(a)->done, 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t + 1u == gridDim.x) {
+            const uint32_t nd = __hip_atomic_load(&acc_cur(a)->ndefer, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (nd) {
+                __threadfence();   // acquire: the deferring waves' entries and outputs
+                repair_deferred<kEmit>(a, nd, lane, Repair{L1[1], L1[2], L1[7], L1[8]});
+            }
+        }
+    }
+
     // ---- rule_stats of mid-size tables: into one of kStatReps replicas of the per-sorted-index
     // totals (the host sums them and credits rule_id; nothing in this launch reads them), so
-    // that the hot rules' counters take 1/kStatReps of the workgroups' atomics each ----
-    if (lds_stats && !small_stats && !(kAblate & 4)) {
+    // that the hot rules' counters take 1/kStatReps of the workgroups' atomics each (by every
+    // wave but the counting one) ----
+    if (lds_stats && !small_stats && !(kAblate & 4) && !(counting && kWaves > 1 && wave == kCounter)) {
         unsigned long long* rep = a.stats_idx + (size_t)(blockIdx.x % kStatReps) * 2 * a.nrules_pad;
-        for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) {
+        const uint32_t skip = counting && kWaves > 1 ? 64u : 0u;
+        const uint32_t t0 = (uint32_t)tid - (counting && kWaves > 1 && wave > kCounter ? 64u : 0u);
+        for (uint32_t k = t0; k < 2 * a.nrules_pad; k += kBlock - skip) {
             const uint32_t v = lds_hist[k];
             if (v) atomicAdd(&rep[k], (unsigned long long)v);
         }
@@ -1869,7 +2003,13 @@ struct upe_gpu_ctx {
     uint32_t paycap = 0;           // largest grid
     // per-batch scratch
     uint32_t* lb = nullptr;        // [tiles_alloc * kWaves] look-back flags (zeroed at allocation)
+    uint32_t* defer = nullptr;     // [64 * tiles_alloc * kWaves] deferred look-back candidates
     size_t tiles_alloc = 0;
+    uint32_t lb_spin = 5000;       // look-back wait before deferring (UPE_GPU_LB_SPIN, 100 MHz ticks)
+    bool lb_sync = false;          // UPE_GPU_LB_SYNC=1: wait for each launch's agreement report
+    bool allow_nolb = true;        // UPE_GPU_NOLB=0: never use the kernels without look-back
+    int last_var = -1;             // kernel variant of the last classify launch
+    uint32_t last_grid = 0;
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
@@ -1899,7 +2039,8 @@ struct upe_gpu_ctx {
         bool busy = false;
         uint64_t lo = 0, wb = 0;   // host byte range the slot's copy-back writes
     };
-    HostSlot hs[3];
+    HostSlot hs[8];
+    uint32_t host_slots = 4;       // device slots of the host round trip (UPE_GPU_HOST_SLOTS, 2..8)
     // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
     // device into host-mapped memory, and the first launch whose report counts
     unsigned long long* agree_h = nullptr;
@@ -1988,11 +2129,14 @@ int publish(upe_gpu_ctx* c) {
 int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
     if (ntiles > c->tiles_alloc) {
         if (c->lb) (void)hipFree(c->lb);
+        if (c->defer) (void)hipFree(c->defer);
         c->lb = nullptr;
+        c->defer = nullptr;
         c->tiles_alloc = 0;
         size_t want = ntiles + ntiles / 4 + 16;
         HIP_TRY(hipMalloc(&c->lb, want * kWaves * sizeof(uint32_t)));
         HIP_TRY(hipMemset(c->lb, 0, want * kWaves * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&c->defer, 64 * want * kWaves * sizeof(uint32_t)));
         c->tiles_alloc = want;
         if (publish(c) != 0) return -1;
     }
@@ -2056,18 +2200,6 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-// A look-back that gave up means the persistent grid was not resident: report it once.
-int check_lookback(upe_gpu_ctx* c) {
-    uint32_t t = 0;
-    HIP_TRY(hipMemcpy(&t, &c->st->lb_timeout, sizeof t, hipMemcpyDeviceToHost));
-    if (t) {
-        HIP_TRY(hipMemset(&c->st->lb_timeout, 0, sizeof t));
-        return fail("a look-back wait gave up: the persistent grid was not resident "
-                    "(results of that batch are not exact)");
-    }
-    return 0;
-}
-
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only).
 constexpr int kVarCount = 16;
 int classify_var(bool tss, bool emit, bool lean, bool nolb) {
@@ -2106,7 +2238,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
 // launch the first time the configuration is used (census_probe).  0 on error.
 uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
-    const uint64_t key = (uint64_t)lds << 3 | (uint64_t)var;
+    static_assert(kVarCount <= 16, "the variant takes the key's low 4 bits");
+    const uint64_t key = (uint64_t)lds << 4 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
     int per_cu = 0;
@@ -2166,6 +2299,68 @@ int upe_gpu_device_count(void) {
     return n;
 }
 
+// The host CPUs local to a GPU: the device's PCI function in sysfs names its NUMA node and the
+// CPUs attached to it (local_cpulist), kept in the calling thread's allowed set.
+int upe_gpu_local_cpus(int device, int* cpus, size_t cap, int* numa_node) {
+    char bus[64] = {0};
+    HIP_TRY(hipDeviceGetPCIBusId(bus, (int)sizeof bus, device));
+    for (char* p = bus; *p; ++p) *p = (char)tolower((unsigned char)*p);
+    const std::string dir = std::string("/sys/bus/pci/devices/") + bus;
+    int node = -1;
+    if (FILE* f = fopen((dir + "/numa_node").c_str(), "r")) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    if (numa_node) *numa_node = node;
+    std::string list;
+    if (FILE* f = fopen((dir + "/local_cpulist").c_str(), "r")) {
+        char buf[4096];
+        if (fgets(buf, sizeof buf, f)) list = buf;
+        fclose(f);
+    }
+    if (list.empty()) return fail("no local_cpulist for PCI device " + std::string(bus));
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return fail("sched_getaffinity failed");
+    size_t n = 0;
+    const char* p = list.c_str();
+    while (*p) {   // "0-63,128-191"
+        char* e = nullptr;
+        const long lo = strtol(p, &e, 10);
+        if (e == p) break;
+        long hi = lo;
+        p = e;
+        if (*p == '-') {
+            hi = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = lo; c <= hi; ++c)
+            if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) {
+                if (cpus && n < cap) cpus[n] = (int)c;
+                ++n;
+            }
+        while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+    }
+    return (int)n;
+}
+
+// Pin the calling thread to one CPU local to `device` (the slot-th of them, modulo their
+// number) — the reference pins each worker thread with affinity_pin_self (src/affinity.c:48,
+// cores from assign_cores, src/main.c:143-175); a GPU worker's host thread belongs on the GPU's
+// NUMA node, where its pinned buffers are then allocated.  Returns the CPU.
+int upe_gpu_pin_self(int device, int slot) {
+    std::vector<int> cpus(CPU_SETSIZE);
+    const int n = upe_gpu_local_cpus(device, cpus.data(), cpus.size(), nullptr);
+    if (n <= 0) return n == 0 ? fail("no allowed CPU is local to the device") : -1;
+    const int cpu = cpus[(size_t)(slot < 0 ? 0 : slot) % (size_t)n];
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(cpu, &one);
+    if (pthread_setaffinity_np(pthread_self(), sizeof one, &one) != 0)
+        return fail("pthread_setaffinity_np failed");
+    return cpu;
+}
+
 upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
     if (rule_capacity == 0 || rule_capacity > (1u << 24)) {
         fail("rule_capacity must be in [1, 2^24]");
@@ -2200,6 +2395,14 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
                 hipSuccess && cus > 0)
             c->cus = cus;
         if (const char* v = getenv("UPE_GPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = atoi(v);
+        // diagnostics: the look-back wait before deferring (0 = defer whenever a flag is not yet
+        // published), a synchronous agreement report per launch (the switch to the kernel without
+        // look-back then happens at a deterministic launch), no kernel without look-back
+        if (const char* v = getenv("UPE_GPU_LB_SPIN")) c->lb_spin = (uint32_t)strtoul(v, nullptr, 10);
+        if (const char* v = getenv("UPE_GPU_LB_SYNC")) c->lb_sync = v[0] == '1';
+        if (const char* v = getenv("UPE_GPU_NOLB")) c->allow_nolb = v[0] != '0';
+        if (const char* v = getenv("UPE_GPU_HOST_SLOTS"))
+            c->host_slots = std::min(8u, std::max(2u, (uint32_t)strtoul(v, nullptr, 10)));
     }
     // payload slots for the largest grid a launch uses (at most 8 workgroups per CU)
     c->paycap = 8u * (uint32_t)c->cus;
@@ -2258,6 +2461,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
                     c->hist_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (c->defer) (void)hipFree(c->defer);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     for (auto& sl : c->hs) {
@@ -2776,6 +2980,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.paycap = c->paycap;
     a.k6 = (uint32_t)(c->k % 6);
     a.lb = c->lb;
+    a.defer = c->defer;
+    a.lb_spin = c->lb_spin;
     a.lb_tag = (uint32_t)(c->k % kLbTagMod) + 1u;
     if (c->k > 0 && c->k % kLbTagMod == 0)   // tags wrap: no flag may carry this launch's tag
         HIP_TRY(hipMemsetAsync(c->lb, 0, c->tiles_alloc * kWaves * sizeof(uint32_t), s));
@@ -2823,7 +3029,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
                       (arp_slots == 0 || a.arp_lds != 0) && (ndp_slots == 0 || a.ndp_lds != 0);
     // once a launch has been seen starting from agreeing L1 entries (or from an entry whose
     // family's index is empty), every later one does until the host changes tables or entries
-    if (!c->no_lb && c->agree_h) {
+    if (!c->no_lb && c->agree_h && c->allow_nolb) {
+        if (c->lb_sync && c->k > c->lb_reset_k && c->last_stream)
+            HIP_TRY(hipStreamSynchronize(c->last_stream));   // the previous launch's report
         const unsigned long long v = __atomic_load_n(c->agree_h, __ATOMIC_ACQUIRE);
         const unsigned long long tag = v >> 2;
         if (tag != 0 && tag - 1 >= c->lb_reset_k && ((v & 1) || c->arp_bits == 0) &&
@@ -2851,6 +3059,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     const uint32_t grid = a.ntiles == 0 ? 1u : a.ntiles < grid_cap ? a.ntiles : grid_cap;
     launch_classify(var, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
+    c->last_var = var;
+    c->last_grid = grid;
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
         // kHistChunkMin) while the grid has fewer than about kHistTarget workgroups
@@ -2960,7 +3170,7 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         if (hi > frames_bytes)
             return fail("a frame window runs past frames_bytes (UPE_FRAME_TAIL bytes must follow "
                         "every frame start)");
-        auto& sl = c->hs[k % 3];
+        auto& sl = c->hs[k % c->host_slots];
         if (sl.busy) HIP_TRY(hipEventSynchronize(sl.out_done));   // the slot's last D2H is done
         sl.busy = false;
         const size_t span = (size_t)(hi - lo);
@@ -3254,7 +3464,7 @@ int upe_gpu_sync(upe_gpu_ctx_t* c, void* stream) {
     if (!c) return fail("null context");
     DEV_SCOPE(c->device);
     HIP_TRY(hipStreamSynchronize(pick(c, stream)));
-    return check_lookback(c);
+    return 0;
 }
 
 int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
@@ -3278,12 +3488,25 @@ int upe_gpu_batch_info(upe_gpu_ctx_t* c, upe_batch_info_t* info) {
     return 0;
 }
 
+int upe_gpu_launch_info(upe_gpu_ctx_t* c, upe_launch_info_t* info) {
+    if (!c || !info) return fail("null argument");
+    DEV_SCOPE(c->device);
+    HIP_TRY(hipDeviceSynchronize());
+    memset(info, 0, sizeof *info);
+    info->launches = c->k;
+    if (c->k == 0 || c->last_var < 0) return 0;
+    info->variant = (uint32_t)c->last_var;
+    info->grid = c->last_grid;
+    HIP_TRY(hipMemcpy(&info->deferred, &acc_slot(c, c->k + 2)->ndefer, sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_t* rule_stats,
                       size_t capacity) {
     if (!c) return fail("null context");
     DEV_SCOPE(c->device);
     HIP_TRY(hipDeviceSynchronize());
-    if (check_lookback(c) != 0) return -1;
     if (counters) {
         // the totals up to batch k - 2, plus batch k - 1 (folded in by the next launch)
         unsigned long long t[8];

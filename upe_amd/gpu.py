@@ -16,11 +16,14 @@ import os
 
 import numpy as np
 
-from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, L1_DTYPE, NDP_DTYPE,
-                     RULE_DTYPE, RULE_STAT_DTYPE)
+from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, L1_DTYPE, LAUNCH_INFO_DTYPE,
+                     NDP_DTYPE, RULE_DTYPE, RULE_STAT_DTYPE)
 
 LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")  # override: diagnostic builds only
+
+
+VAR_NOLB = 8   # launch_info variant bit: the kernel without look-back
 
 
 class UpeGpuError(RuntimeError):
@@ -36,6 +39,8 @@ def _load() -> ctypes.CDLL:
     sig = {
         "upe_gpu_last_error": (ctypes.c_char_p, []),
         "upe_gpu_device_count": (I, []),
+        "upe_gpu_local_cpus": (I, [I, P, SZ, P]),
+        "upe_gpu_pin_self": (I, [I, I]),
         "upe_gpu_open": (P, [I, SZ]),
         "upe_gpu_close": (None, [P]),
         "upe_gpu_load_rules": (I, [P, P, SZ]),
@@ -47,6 +52,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process": (I, [P, P, P, P, SZ, P]),
         "upe_gpu_sync": (I, [P, P]),
         "upe_gpu_batch_info": (I, [P, P]),
+        "upe_gpu_launch_info": (I, [P, P]),
         "upe_gpu_get_stats": (I, [P, P, P, SZ]),
         "upe_gpu_reset_stats": (I, [P]),
         "upe_gpu_timing_enable": (I, [P, I]),
@@ -73,6 +79,8 @@ def _load() -> ctypes.CDLL:
         "upe_host_last_error": (ctypes.c_char_p, []),
     })
     for name, (res, args) in sig.items():
+        if os.environ.get("UPE_GPU_LIB_DIAG") and not hasattr(lib, name):
+            continue   # an older diagnostic build (A/B timing) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -82,9 +90,11 @@ def _load() -> ctypes.CDLL:
 LIB = _load()
 
 # every symbol include/upe_gpu.h declares (checked by tests/test_abi.py)
-EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_open", "upe_gpu_close",
+EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", "upe_gpu_pin_self",
+            "upe_gpu_open", "upe_gpu_close",
             "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
             "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
+            "upe_gpu_launch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_span",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
@@ -117,6 +127,24 @@ def _dev_ptr(x) -> int:
 
 def device_count() -> int:
     return LIB.upe_gpu_device_count()
+
+
+def local_cpus(device: int):
+    """(CPUs local to the GPU that this thread may use, NUMA node) — upe_gpu_local_cpus."""
+    buf = np.zeros(4096, np.int32)
+    node = ctypes.c_int(-1)
+    n = LIB.upe_gpu_local_cpus(device, _np_ptr(buf), buf.size, ctypes.byref(node))
+    if n < 0:
+        raise UpeGpuError(f"upe_gpu_local_cpus: {LIB.upe_gpu_last_error().decode()}")
+    return [int(x) for x in buf[:min(n, buf.size)]], node.value
+
+
+def pin_self(device: int, slot: int = 0) -> int:
+    """Pin the calling thread to a CPU local to the GPU (upe_gpu_pin_self); returns the CPU."""
+    cpu = LIB.upe_gpu_pin_self(device, slot)
+    if cpu < 0:
+        raise UpeGpuError(f"upe_gpu_pin_self: {LIB.upe_gpu_last_error().decode()}")
+    return cpu
 
 
 class GpuWorker:
@@ -255,6 +283,13 @@ class GpuWorker:
         x = np.zeros(1, BATCH_INFO_DTYPE)
         _check(LIB.upe_gpu_batch_info(self._ctx, _np_ptr(x)), "upe_gpu_batch_info")
         return x
+
+    def launch_info(self) -> dict:
+        """upe_gpu_launch_info: the last classify launch's kernel variant (bit 3 = no look-back),
+        grid, deferred look-back entries, and the context's launch count."""
+        x = np.zeros(1, LAUNCH_INFO_DTYPE)
+        _check(LIB.upe_gpu_launch_info(self._ctx, _np_ptr(x)), "upe_gpu_launch_info")
+        return {k: int(x[k][0]) for k in LAUNCH_INFO_DTYPE.names}
 
     def get_stats(self):
         c = np.zeros(1, COUNTERS_DTYPE)
