@@ -204,28 +204,37 @@ def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
             "sample": sample}
 
 
-def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
+def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool, apply_threads=None) -> dict:
     """Host-inclusive rate: the batch starts and ends in pinned host memory (libpcap in, AF_PACKET
-    out): upe_gpu_process_host pipelines H2D of frames + descriptors, classify and D2H of verdicts
-    + rewritten header bytes over chunks.  windows: ship 96-byte header windows, not frames."""
+    out).  In place (apply_threads None): upe_gpu_process_host pipelines H2D of frames +
+    descriptors, classify and D2H of verdicts + the rewritten header span over chunks.  Emit:
+    upe_gpu_process_host_emit brings back verdicts + 16-byte records and applies them to the
+    frames on the host with 1 + apply_threads threads (the same output bytes).  windows: ship
+    96-byte header windows, not frames."""
     from upe_amd import gpu, synth
     from upe_amd.layout import FRAME_TAIL, REWRITE_EXTENT, desc_lens, desc_offsets
 
     src = synth.header_windows(wl) if windows else wl
+    emit = apply_threads is not None
     pf = gpu.PinnedArray(src.frames.shape, np.uint8)
     pd = gpu.PinnedArray(src.desc.shape, np.uint64)
     pv = gpu.PinnedArray((wl.n,), np.uint32)
+    ph = gpu.PinnedArray((wl.n, 16), np.uint8) if emit else None
     pd.array[:] = src.desc
     times = []
     for r in range(reps + 2):
         pf.array[:] = src.frames          # untimed: a fresh batch every pass
         t0 = time.perf_counter()
-        worker.process_host(pf.array, pd.array, pv.array, chunk)
+        if emit:
+            worker.process_host_emit(pf.array, pd.array, pv.array, ph.array, chunk, apply_threads)
+        else:
+            worker.process_host(pf.array, pd.array, pv.array, chunk)
         t1 = time.perf_counter()
         if r >= 2:
             times.append(t1 - t0)
-    for x in (pf, pd, pv):
-        x.free()
+    for x in (pf, pd, pv, ph):
+        if x is not None:
+            x.free()
     t = float(np.median(times))
     # bytes the copies actually move: per chunk the frame span in, and back the span up to the
     # last rewritable byte (UPE_REWRITE_EXTENT) plus the verdicts
@@ -236,9 +245,11 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool) -> dict:
     for s in range(0, wl.n, ck):
         o, ln = offs[s:s + ck], lens[s:s + ck]
         h2d += int(o.max() + FRAME_TAIL - o.min()) + 8 * len(o)
-        d2h += int((o + np.minimum(ln, REWRITE_EXTENT)).max() - o.min()) + 4 * len(o)
+        d2h += (20 * len(o) if emit else
+                int((o + np.minimum(ln, REWRITE_EXTENT)).max() - o.min()) + 4 * len(o))
     return {"seconds": t, "packets": wl.n, "h2d_bytes": h2d, "d2h_bytes": d2h,
-            "windows": windows, "chunk": chunk or (1 << 18), "reps": reps}
+            "windows": windows, "chunk": chunk or (1 << 18), "reps": reps,
+            "times": times, "emit": emit, "apply_threads": apply_threads}
 
 
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
@@ -326,6 +337,11 @@ def main() -> None:
                          "classify -> D2H), after every timed leg; 0 skips it.  Its launches "
                          "are a separate leg of a rocprof trace (tools/kernel_legs.py)")
     ap.add_argument("--host-chunk", type=int, default=0)
+    ap.add_argument("--host-apply-threads", type=int, default=7,
+                    help="pool threads (besides the calling one) applying the records of the "
+                         "emit-mode host round trip; -1: records returned, not applied")
+    ap.add_argument("--no-host-emit", action="store_true",
+                    help="skip the emit-mode host round trip")
     ap.add_argument("--workers-per-gpu", type=int, default=0,
                     help="also time W worker contexts sharing this GPU, each on its own stream "
                          "with its own batches and L1 state, as W reference worker threads would "
@@ -489,18 +505,26 @@ def main() -> None:
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
     worker.reset_stats()
-    hr = None
+    hr = hre = None
     if args.host_reps > 0:
         if dist:
             dist.barrier()
         hr = host_roundtrip(worker, wl, args.host_reps, args.host_chunk,
                             windows=args.config != "B")
+        if not args.no_host_emit:
+            worker.reset_stats()
+            if dist:
+                dist.barrier()
+            hre = host_roundtrip(worker, wl, args.host_reps, args.host_chunk,
+                                 windows=args.config != "B", apply_threads=args.host_apply_threads)
 
     # the job ends when the slowest shard does; value = every rank's packets / that time
     elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
     total_packets = float(shard.sum_over_ranks([n * args.steps], dist, dev)[0])
     if hr:
         hr["seconds"] = shard.max_over_ranks(hr["seconds"], dist, dev)
+    if hre:
+        hre["seconds"] = shard.max_over_ranks(hre["seconds"], dist, dev)
 
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first, emit=args.mode == "emit")
@@ -566,19 +590,30 @@ def main() -> None:
             out["imix"] = imix
         if shared:
             out["workers_sharing_gpu"] = shared
+        def host_line(h, what):
+            return {"value": round(h["packets"] * world / h["seconds"] / 1e6, 2), "unit": "Mpps",
+                    "ms_per_batch": round(h["seconds"] * 1e3, 3),
+                    "ms_min_max": [round(min(h["times"]) * 1e3, 3), round(max(h["times"]) * 1e3, 3)],
+                    "h2d_GBps": round(h["h2d_bytes"] / h["seconds"] / 1e9, 2),
+                    "d2h_GBps": round(h["d2h_bytes"] / h["seconds"] / 1e9, 2),
+                    "h2d_bytes_per_packet": round(h["h2d_bytes"] / h["packets"], 1),
+                    "d2h_bytes_per_packet": round(h["d2h_bytes"] / h["packets"], 1),
+                    "header_windows": h["windows"], "chunk": h["chunk"],
+                    "what": what + f"; median of {h['reps']} passes, all ranks at once"}
+
         if hr:
-            out["host_roundtrip"] = {
-                "value": round(hr["packets"] * world / hr["seconds"] / 1e6, 2), "unit": "Mpps",
-                "ms_per_batch": round(hr["seconds"] * 1e3, 3),
-                "h2d_GBps": round(hr["h2d_bytes"] / hr["seconds"] / 1e9, 2),
-                "d2h_GBps": round(hr["d2h_bytes"] / hr["seconds"] / 1e9, 2),
-                "h2d_bytes_per_packet": round(hr["h2d_bytes"] / hr["packets"], 1),
-                "d2h_bytes_per_packet": round(hr["d2h_bytes"] / hr["packets"], 1),
-                "header_windows": hr["windows"], "chunk": hr["chunk"],
-                "what": "pinned host batch -> H2D -> classify -> D2H of verdicts + rewritten "
-                        "header bytes, 3-slot pipeline (upe_gpu_process_host); median of "
-                        f"{hr['reps']} passes, all ranks at once",
-            }
+            out["host_roundtrip"] = host_line(
+                hr, "pinned host batch -> H2D -> classify -> D2H of verdicts + the rewritten "
+                    "header span, frames rewritten in place (upe_gpu_process_host), "
+                    "4-slot pipeline")
+        if hre:
+            out["host_roundtrip_emit"] = host_line(
+                hre, "pinned host batch -> H2D -> classify (emit) -> D2H of verdicts + 16-B "
+                     "records (upe_gpu_process_host_emit), " +
+                     (f"applied to the frames on the host by {1 + hre['apply_threads']} threads: "
+                      "the same output bytes as host_roundtrip" if hre["apply_threads"] >= 0 else
+                      "not applied (frames untouched: a TX path sends each record as its own "
+                      "iovec)"))
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             # config A is the reference's one-worker pcap replay: time it on one core
             out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads,

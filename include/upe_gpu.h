@@ -180,9 +180,9 @@ const char *upe_gpu_last_error(void);
 /* Number of visible GPUs, or -1. */
 int upe_gpu_device_count(void);
 
-/* Host CPUs local to a GPU (its PCI function's NUMA node, sysfs local_cpulist) that the calling
- * thread may run on: up to `cap` of them into cpus (may be NULL), *numa_node (may be NULL) = the
- * node or -1.  Returns how many there are, or -1. */
+/* Host CPUs local to a GPU (its PCI function's NUMA node, sysfs local_cpulist) that the process
+ * may run on (its affinity when the library was loaded): up to `cap` of them into cpus (may be
+ * NULL), *numa_node (may be NULL) = the node or -1.  Returns how many there are, or -1. */
 int upe_gpu_local_cpus(int device, int *cpus, size_t cap, int *numa_node);
 
 /* Pin the calling thread to the slot-th CPU local to `device` (modulo their number), as the
@@ -262,7 +262,7 @@ void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec);
 /* Host round trip: process n packets that live in HOST memory, the way the path runs between
  * libpcap (reference src/rx_pcap.c:42-93 fills pktbufs in host memory) and AF_PACKET TX
  * (src/tx_afpacket.c:78-118 sends from host memory).  The batch is cut into chunks of `chunk`
- * packets (0 = 256k) pipelined through three device slots: chunk k+1's frames and descriptors go
+ * packets (0 = 256k) pipelined through a ring of device slots (4; UPE_GPU_HOST_SLOTS): chunk k+1's frames and descriptors go
  * host->device on a copy stream while chunk k is classified on the context's stream and chunk
  * k-1's verdicts and rewritten header bytes go device->host on a second copy stream.  Chunks are
  * classified in order, so counters, rule_stats and the L1 state evolve exactly as for
@@ -276,6 +276,20 @@ void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec);
 #define UPE_REWRITE_EXTENT 48
 int upe_gpu_process_host(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_bytes,
                          const uint64_t *h_desc, uint32_t *h_verdict, size_t n, size_t chunk);
+
+/* The host round trip in emit mode: the same pipeline, but only the verdicts and the 16-byte
+ * rewritten-header records come back (h_hdr, n records, pinned for the full rate: 20 bytes per
+ * packet over the link instead of the frames' rewritten span — the link's two directions share
+ * its bandwidth, so fewer bytes back let the frames go in faster).  apply_threads >= 0: the
+ * records are applied to h_frames on the host (upe_hdr_apply, answered ARP requests copied back)
+ * by the calling thread plus `apply_threads` pool threads pinned near the GPU, two chunks behind
+ * the copies, so that on return h_frames, h_verdict, counters, rule_stats and the L1 state are
+ * exactly those of upe_gpu_process_host(); apply_threads = -1 leaves the frames as they were
+ * except the answered ARP requests (as upe_gpu_process_emit does; a TX path that sends each
+ * record as its own iovec).  Synchronous.  0 / -1. */
+int upe_gpu_process_host_emit(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_bytes,
+                              const uint64_t *h_desc, uint32_t *h_verdict, upe_hdr_rec_t *h_hdr,
+                              size_t n, size_t chunk, int apply_threads);
 
 /* Pinned (page-locked) host memory for upe_gpu_process_host() batches. */
 void *upe_gpu_host_alloc(size_t bytes);

@@ -67,6 +67,11 @@
 #include <atomic>
 #include <new>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/upe_gpu.h"
@@ -123,6 +128,29 @@ constexpr int kReps = 32;              // replicas of the per-batch accumulators
 // 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 256 no fold of the
 // previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
+// Header windows in two steps (bytes 48..79 only for frames that need them): 0 off, 1 the rest
+// requested when the window is consumed, 2 at the end of the chunk before (diagnostic builds)
+#ifndef UPE_WIN48
+#define UPE_WIN48 0
+#endif
+constexpr int kWin48 = UPE_WIN48;
+// Cache-policy bits of the emit-mode record store (buffer aux: 1 sc0, 2 nt, 16 sc1; 0 = a plain
+// store).  sc1 writes the records through and drops their lines from the XCD's L2, so the end
+// of a launch has ~16 MB less dirty data to write back at the kernel boundary: config B
+// 24.5 -> 24.1 us per 1M batch (nt 24.5, sc0 sc1 24.2, nt sc1 24.2).
+#ifndef UPE_REC_AUX
+#define UPE_REC_AUX 16
+#endif
+constexpr int kRecAux = UPE_REC_AUX;
+// The verdict words written through too (one dword per lane, coalesced): B 24.25 -> 24.1 us.
+// In-place header stores written through (UPE_FRAME_SC1) were slower: 33.7 -> 35.4 us.
+#ifndef UPE_VERDICT_SC1
+#define UPE_VERDICT_SC1 1
+#endif
+constexpr bool kVerdictSc1 = UPE_VERDICT_SC1;
+#ifndef UPE_FRAME_SC1
+#define UPE_FRAME_SC1 0
+#endif
 #ifndef UPE_DIAG_NO_DONE
 #define UPE_DIAG_NO_DONE 0   // diagnostic timing builds only: no deferred-candidate repair
 #endif
@@ -399,6 +427,16 @@ __device__ __forceinline__ uint32_t csum_fold(unsigned long long sum) {
     return (~f) & 0xFFFFu;
 }
 __device__ __forceinline__ void store16(uint4* p, uint4 v) { *p = v; }
+// The in-place header stores (diagnostic UPE_FRAME_SC1: written through, lines dropped from L2).
+__device__ __forceinline__ void store16_frame(uint4* p, uint4 v) {
+#if UPE_FRAME_SC1
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+#else
+    *p = v;
+#endif
+}
 
 // ---- neighbour lookups ----------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t fold_v6(const uint32_t ip[4]) {
@@ -1140,10 +1178,24 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
             v.c0 = q[0]; v.c1 = q[1]; v.c2 = q[2];
-            if (len > 48u) v.c3 = q[3];
-            if (len > 64u) v.c4 = q[4];
+            if (!kWin48) {
+                if (len > 48u) v.c3 = q[3];
+                if (len > 64u) v.c4 = q[4];
+            }
         }
         return v;
+    };
+    // kWin48: bytes 48..79 only for the frames that use them.  An option-less IPv4 frame (byte 14
+    // 0x45) needs bytes 0..46 on every path (the TCP data offset is byte 46); IPv6, IPv4 with
+    // options, ARP and the rest take bytes 48..79 once bytes 12..14 have arrived.
+    auto fetch_rest = [&](uint64_t dsc, bool live, uint4 c0, uint4& c3, uint4& c4) {
+        const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
+        const bool opt4 = (c0.w & 0xFFFFFFu) == 0x450008u;   // bytes 12..14: 08 00 45
+        if (live && len > 48u && !opt4) {
+            const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
+            c3 = q[3];
+            if (len > 64u) c4 = q[4];
+        }
     };
     Win nw;
     bool have_nw = false;   // nw holds the window of the wave's next chunk
@@ -1291,6 +1343,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint8_t* p = a.frames + ((size_t)off16 << 4);
         uint32_t w[20];
         if (kMid && have_nw) {
+            if (kWin48 == 1) fetch_rest(dsc, live, nw.c0, nw.c3, nw.c4);
             const uint4 c[5] = {nw.c0, nw.c1, nw.c2, nw.c3, nw.c4};
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
@@ -1524,15 +1577,28 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
                              : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
             }
-            a.hdr[i] = rec;
+            if (kRecAux == 0) {
+                a.hdr[i] = rec;
+            } else {   // diagnostic: the record store with cache-policy bits (UPE_REC_AUX)
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.hdr, 0, 0x7FFFFFF0, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{rec.x, rec.y, rec.z, rec.w}, rs, i * 16u, 0,
+                                                       kRecAux);
+            }
         } else if (live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
-                store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
-                                          (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
-            if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
+                store16_frame(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
+                                                (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
+            if (wrote1) store16_frame(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
-        if (live) a.verdict[i] = code | flags | rbits;
+        if (live) {
+            if (kVerdictSc1)   // written through (sc1): no dirty lines left for the boundary
+                __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                a.verdict[i] = code | flags | rbits;
+        }
         // 2 B/packet for upe_rule_hist (lean linear-scan launches never have the array; the
         // tuple-space tables it serves always do)
         if ((kTssMode || !kLean) && a.lens16 && live) a.lens16[i] = (uint16_t)len;
@@ -1589,6 +1655,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
             }
         }
+        if (kMid && kWin48 == 2 && have_nw)
+            fetch_rest(dsc_next, chn * 64u + (uint32_t)lane < a.n, nw.c0, nw.c3, nw.c4);
         if (late) {
             chn = claim();
             dsc_next = 0;
@@ -1952,6 +2020,65 @@ __global__ void __launch_bounds__(256) upe_ctrl_gather(const uint8_t* frames, co
 
 }  // namespace
 
+// A small pool of host threads that run one job over slices: job(slice, slices), the caller
+// being slice 0 (upe_gpu_process_host_emit applies the returned records to the caller's frames
+// with it while later chunks are on the link).  Threads are pinned to the GPU's NUMA-local CPUs.
+struct ApplyPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::function<void(unsigned, unsigned)> job;
+    uint64_t gen = 0;
+    unsigned left = 0;
+    bool stop = false;
+
+    ApplyPool(unsigned n, const std::vector<int>& cpus) {
+        for (unsigned t = 0; t < n; ++t)
+            th.emplace_back([this, t, n, cpus] {
+                if (!cpus.empty()) {   // after the caller's CPU (local slot 0)
+                    cpu_set_t one;
+                    CPU_ZERO(&one);
+                    CPU_SET(cpus[(1 + t) % cpus.size()], &one);
+                    (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+                }
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(unsigned, unsigned)> f;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        go.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        f = job;
+                    }
+                    f(t + 1, n + 1);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--left == 0) done.notify_one();
+                }
+            });
+    }
+    ~ApplyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto& t : th) t.join();
+    }
+    void run(const std::function<void(unsigned, unsigned)>& f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = f;
+            left = (unsigned)th.size();
+            ++gen;
+        }
+        go.notify_all();
+        f(0, (unsigned)th.size() + 1);
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return left == 0; });
+    }
+};
+
 struct upe_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2034,12 +2161,15 @@ struct upe_gpu_ctx {
         size_t frames_cap = 0;
         uint64_t* desc = nullptr;
         uint32_t* verdict = nullptr;
+        upe_hdr_rec_t* hdr = nullptr;   // emit-mode records (upe_gpu_process_host_emit)
         size_t pk_cap = 0;
         hipEvent_t in_done = nullptr, k_done = nullptr, out_done = nullptr;
         bool busy = false;
         uint64_t lo = 0, wb = 0;   // host byte range the slot's copy-back writes
     };
     HostSlot hs[8];
+    // host threads applying emit-mode records to the caller's frames (upe_gpu_process_host_emit)
+    std::unique_ptr<struct ApplyPool> pool;
     uint32_t host_slots = 4;       // device slots of the host round trip (UPE_GPU_HOST_SLOTS, 2..8)
     // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
     // device into host-mapped memory, and the first launch whose report counts
@@ -2299,8 +2429,17 @@ int upe_gpu_device_count(void) {
     return n;
 }
 
+// The process's allowed CPUs as they were when the library was loaded (before any thread of it
+// was pinned: a pinned thread's own mask is one CPU).
+static cpu_set_t g_process_cpus;
+__attribute__((constructor)) static void upe_capture_cpus() {
+    CPU_ZERO(&g_process_cpus);
+    if (sched_getaffinity(0, sizeof g_process_cpus, &g_process_cpus) != 0)
+        for (int c = 0; c < CPU_SETSIZE; ++c) CPU_SET(c, &g_process_cpus);
+}
+
 // The host CPUs local to a GPU: the device's PCI function in sysfs names its NUMA node and the
-// CPUs attached to it (local_cpulist), kept in the calling thread's allowed set.
+// CPUs attached to it (local_cpulist), kept in the process's allowed set.
 int upe_gpu_local_cpus(int device, int* cpus, size_t cap, int* numa_node) {
     char bus[64] = {0};
     HIP_TRY(hipDeviceGetPCIBusId(bus, (int)sizeof bus, device));
@@ -2319,9 +2458,7 @@ int upe_gpu_local_cpus(int device, int* cpus, size_t cap, int* numa_node) {
         fclose(f);
     }
     if (list.empty()) return fail("no local_cpulist for PCI device " + std::string(bus));
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return fail("sched_getaffinity failed");
+    const cpu_set_t& allowed = g_process_cpus;
     size_t n = 0;
     const char* p = list.c_str();
     while (*p) {   // "0-63,128-191"
@@ -2465,7 +2602,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     for (auto& sl : c->hs) {
-        for (void* b : {(void*)sl.frames, (void*)sl.desc, (void*)sl.verdict})
+        for (void* b : {(void*)sl.frames, (void*)sl.desc, (void*)sl.verdict, (void*)sl.hdr})
             if (b) (void)hipFree(b);
         for (hipEvent_t e : {sl.in_done, sl.k_done, sl.out_done})
             if (e) (void)hipEventDestroy(e);
@@ -3122,10 +3259,21 @@ int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_
     return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
 }
 
-int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
-                         const uint64_t* h_desc, uint32_t* h_verdict, size_t n, size_t chunk) {
+}  // extern "C"
+
+namespace {
+// The host round trip (upe_gpu_process_host / _emit): chunks of the caller's host batch through
+// a ring of device slots, H2D on one copy stream, classify on the context's stream, D2H on a
+// second copy stream.  In place: the rewritten span [lo, wb) of each chunk comes back.  Emit:
+// the verdicts and the 16-byte records come back (20 B per packet instead of the span: the
+// link's two directions share its bandwidth, so fewer bytes back let more go in), and when
+// apply_threads >= 0 the records are applied to the caller's frames on the host two chunks
+// behind, by the calling thread and `apply_threads` pool threads, while later chunks move.
+int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
+                   const uint64_t* h_desc, uint32_t* h_verdict, upe_hdr_rec_t* h_hdr, size_t n,
+                   size_t chunk, bool emit, int apply_threads) {
     if (!c) return fail("null context");
-    if (n && (!h_frames || !h_desc || !h_verdict)) return fail("null host buffer");
+    if (n && (!h_frames || !h_desc || !h_verdict || (emit && !h_hdr))) return fail("null host buffer");
     DEV_SCOPE(c->device);
     if (chunk == 0) chunk = (size_t)1 << 18;
     if (!c->s_in) {
@@ -3142,6 +3290,14 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         HIP_TRY(hipStreamSynchronize(c->stream));
         return 0;
     }
+    const bool apply = emit && apply_threads >= 0;
+    if (apply && apply_threads > 0 && (!c->pool || c->pool->th.size() != (size_t)apply_threads)) {
+        std::vector<int> cpus(CPU_SETSIZE);
+        const int k = upe_gpu_local_cpus(c->device, cpus.data(), cpus.size(), nullptr);
+        cpus.resize(k > 0 ? (size_t)k : 0);
+        c->pool.reset();
+        c->pool.reset(new ApplyPool((unsigned)apply_threads, cpus));
+    }
     // Whatever happens below, no copy into the caller's buffers is left in flight on return.
     struct Drain {
         upe_gpu_ctx* c;
@@ -3152,6 +3308,40 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
             for (auto& sl : c->hs) sl.busy = false;
         }
     } drain{c};
+    const size_t nslots = c->host_slots;
+    const size_t lag = 2;   // emit: chunk k - lag is applied while chunk k is issued
+    struct Done {
+        size_t s, e, slot;
+        uint64_t lo;
+    };
+    std::vector<Done> pending;
+    // apply chunk d's records (and copy back its answered ARP requests, rewritten in place in
+    // the device slot, which the reference transmits from b->data, src/worker.c:40-52)
+    auto finish = [&](const Done& d) -> int {
+        auto& sl = c->hs[d.slot];
+        HIP_TRY(hipEventSynchronize(sl.out_done));
+        std::atomic<bool> replies{false};
+        auto job = [&](unsigned t, unsigned T) {
+            const size_t m = d.e - d.s, a0 = d.s + m * t / T, a1 = d.s + m * (t + 1) / T;
+            bool r = false;
+            for (size_t i = a0; i < a1; ++i) {
+                r |= (h_verdict[i] & UPE_VF_ARP_REPLY) != 0;
+                if (apply && h_hdr[i].b[15]) upe_hdr_apply(h_frames + (h_desc[i] >> 16), &h_hdr[i]);
+            }
+            if (r) replies.store(true, std::memory_order_relaxed);
+        };
+        if (c->pool && apply && apply_threads > 0) c->pool->run(job);
+        else job(0, 1);
+        if (replies.load())
+            for (size_t i = d.s; i < d.e; ++i)
+                if (h_verdict[i] & UPE_VF_ARP_REPLY) {
+                    const uint64_t off = h_desc[i] >> 16, len = h_desc[i] & 0xFFFFu;
+                    HIP_TRY(hipMemcpy(h_frames + off, sl.frames + (off - d.lo),
+                                      len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT,
+                                      hipMemcpyDeviceToHost));
+                }
+        return 0;
+    };
     size_t k = 0;
     for (size_t s = 0; s < n; s += chunk, ++k) {
         const size_t e = n - s < chunk ? n : s + chunk, m = e - s;
@@ -3170,7 +3360,12 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         if (hi > frames_bytes)
             return fail("a frame window runs past frames_bytes (UPE_FRAME_TAIL bytes must follow "
                         "every frame start)");
-        auto& sl = c->hs[k % c->host_slots];
+        const size_t si = k % nslots;
+        auto& sl = c->hs[si];
+        if (emit && pending.size() >= lag) {   // the oldest finished before its slot is reused
+            if (finish(pending.front()) != 0) return -1;
+            pending.erase(pending.begin());
+        }
         if (sl.busy) HIP_TRY(hipEventSynchronize(sl.out_done));   // the slot's last D2H is done
         sl.busy = false;
         const size_t span = (size_t)(hi - lo);
@@ -3182,23 +3377,28 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
             HIP_TRY(hipMalloc(&sl.frames, want));
             sl.frames_cap = want;
         }
-        if (m > sl.pk_cap) {
-            if (sl.desc) HIP_TRY(hipFree(sl.desc));
-            if (sl.verdict) HIP_TRY(hipFree(sl.verdict));
+        if (m > sl.pk_cap || (emit && !sl.hdr)) {
+            for (void* b : {(void*)sl.desc, (void*)sl.verdict, (void*)sl.hdr})
+                if (b) HIP_TRY(hipFree(b));
             sl.desc = nullptr;
             sl.verdict = nullptr;
+            sl.hdr = nullptr;
+            const size_t cap = std::max(m, sl.pk_cap);
             sl.pk_cap = 0;
-            HIP_TRY(hipMalloc(&sl.desc, m * sizeof(uint64_t)));
-            HIP_TRY(hipMalloc(&sl.verdict, m * sizeof(uint32_t)));
-            sl.pk_cap = m;
+            HIP_TRY(hipMalloc(&sl.desc, cap * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&sl.verdict, cap * sizeof(uint32_t)));
+            if (emit) HIP_TRY(hipMalloc(&sl.hdr, cap * sizeof(upe_hdr_rec_t)));
+            sl.pk_cap = cap;
         }
-        // A chunk whose bytes interleave with an earlier chunk's (descriptors in any order, e.g.
-        // pool addresses) must read them only after that chunk's copy-back has landed: its own
-        // copy-back rewrites its whole span, and would otherwise put back the earlier chunk's
-        // frames as they were before they were processed.
-        for (auto& other : c->hs)
-            if (&other != &sl && other.busy && other.lo < hi && lo < other.wb)
-                HIP_TRY(hipStreamWaitEvent(c->s_in, other.out_done, 0));
+        // In place: a chunk whose bytes interleave with an earlier chunk's (descriptors in any
+        // order, e.g. pool addresses) must read them only after that chunk's copy-back has
+        // landed: its own copy-back rewrites its whole span, and would otherwise put back the
+        // earlier chunk's frames as they were before they were processed.  (Emit mode copies
+        // no frame bytes back.)
+        if (!emit)
+            for (auto& other : c->hs)
+                if (&other != &sl && other.busy && other.lo < hi && lo < other.wb)
+                    HIP_TRY(hipStreamWaitEvent(c->s_in, other.out_done, 0));
         HIP_TRY(hipMemcpyAsync(sl.frames, h_frames + lo, span, hipMemcpyHostToDevice, c->s_in));
         HIP_TRY(hipMemcpyAsync(sl.desc, h_desc + s, m * sizeof(uint64_t), hipMemcpyHostToDevice,
                                c->s_in));
@@ -3207,20 +3407,46 @@ int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_byte
         // the descriptors keep their offsets relative to h_frames: hand the kernel a base that
         // maps offset lo onto the slot (lo is a multiple of 16, so the base stays aligned)
         uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.frames) - lo);
-        if (upe_gpu_process(c, base, sl.desc, sl.verdict, m, nullptr) != 0) return -1;
+        if (emit ? upe_gpu_process_emit(c, base, sl.desc, sl.verdict, sl.hdr, m, nullptr)
+                 : upe_gpu_process(c, base, sl.desc, sl.verdict, m, nullptr))
+            return -1;
         HIP_TRY(hipEventRecord(sl.k_done, c->stream));
         HIP_TRY(hipStreamWaitEvent(c->s_out, sl.k_done, 0));
         HIP_TRY(hipMemcpyAsync(h_verdict + s, sl.verdict, m * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, c->s_out));
-        HIP_TRY(hipMemcpyAsync(h_frames + lo, sl.frames, (size_t)(wb - lo), hipMemcpyDeviceToHost,
-                               c->s_out));
+        if (emit)
+            HIP_TRY(hipMemcpyAsync(h_hdr + s, sl.hdr, m * sizeof(upe_hdr_rec_t),
+                                   hipMemcpyDeviceToHost, c->s_out));
+        else
+            HIP_TRY(hipMemcpyAsync(h_frames + lo, sl.frames, (size_t)(wb - lo),
+                                   hipMemcpyDeviceToHost, c->s_out));
         HIP_TRY(hipEventRecord(sl.out_done, c->s_out));
         sl.busy = true;
         sl.lo = lo;
         sl.wb = wb;
+        if (emit) pending.push_back(Done{s, e, si, lo});
     }
+    for (const Done& d : pending)
+        if (finish(d) != 0) return -1;
     HIP_TRY(hipStreamSynchronize(c->s_out));
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int upe_gpu_process_host(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
+                         const uint64_t* h_desc, uint32_t* h_verdict, size_t n, size_t chunk) {
+    return host_roundtrip(c, h_frames, frames_bytes, h_desc, h_verdict, nullptr, n, chunk, false,
+                          -1);
+}
+
+int upe_gpu_process_host_emit(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
+                              const uint64_t* h_desc, uint32_t* h_verdict, upe_hdr_rec_t* h_hdr,
+                              size_t n, size_t chunk, int apply_threads) {
+    if (apply_threads > 64) return fail("apply_threads must be at most 64");
+    return host_roundtrip(c, h_frames, frames_bytes, h_desc, h_verdict, h_hdr, n, chunk, true,
+                          apply_threads);
 }
 
 void* upe_gpu_host_alloc(size_t bytes) {

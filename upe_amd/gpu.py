@@ -63,6 +63,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_memcpy_h2d": (I, [P, P, P, SZ, P]),
         "upe_gpu_memcpy_d2h": (I, [P, P, P, SZ, P]),
         "upe_gpu_process_host": (I, [P, P, SZ, P, P, SZ, SZ]),
+        "upe_gpu_process_host_emit": (I, [P, P, SZ, P, P, P, SZ, SZ, I]),
         "upe_gpu_process_batches": (I, [P, P, P, P, SZ, SZ, P]),
         "upe_gpu_process_rss": (I, [P, P, P, P, P, SZ, P]),
         "upe_gpu_compact": (I, [P, P, SZ, ctypes.c_uint32, P, P, P]),
@@ -99,6 +100,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_gpu_timing_span",
             "upe_gpu_timing_read", "upe_gpu_malloc", "upe_gpu_free",
             "upe_gpu_memcpy_h2d", "upe_gpu_memcpy_d2h", "upe_gpu_process_host",
+            "upe_gpu_process_host_emit",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
             "upe_gpu_process_segmented", "upe_gpu_process_emit", "upe_gpu_process_batches_emit",
             "upe_hdr_apply",
@@ -329,6 +331,20 @@ class GpuWorker:
                                         _np_ptr(verdict) if verdict.size else None,
                                         int(desc.shape[0]), int(chunk)),
                "upe_gpu_process_host")
+
+    def process_host_emit(self, frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray,
+                          hdr: np.ndarray, chunk: int = 0, apply_threads: int = 0) -> None:
+        """upe_gpu_process_host_emit: verdicts + records (hdr, (n, 16) uint8) back; with
+        apply_threads >= 0 the records are applied to `frames` on the host."""
+        assert frames.dtype == np.uint8 and desc.dtype == np.uint64 and verdict.dtype == np.uint32
+        assert hdr.dtype == np.uint8 and hdr.size >= 16 * desc.shape[0]
+        assert verdict.shape[0] >= desc.shape[0]
+        _check(LIB.upe_gpu_process_host_emit(self._ctx, _np_ptr(frames), frames.nbytes,
+                                             _np_ptr(desc) if desc.size else None,
+                                             _np_ptr(verdict) if verdict.size else None,
+                                             _np_ptr(hdr) if hdr.size else None,
+                                             int(desc.shape[0]), int(chunk), int(apply_threads)),
+               "upe_gpu_process_host_emit")
 
     # ---- device memory without torch ----
     def malloc(self, nbytes: int) -> int:
