@@ -17,4 +17,4 @@ for spec in "$@"; do
       || echo "pass $label $c failed rc=$?"
   done
 done
-python tools/pmc_ab_summary.py $cfg
+python tools/pmc_ab_summary.py $cfg $([ "$cfg" = D ] && echo 16777216)

@@ -270,7 +270,17 @@ struct NeighIndex {
 struct __attribute__((aligned(16))) TssGroup {
     uint32_t w[16];
 };
-constexpr int kTssSlot4 = 2, kTssSlot6 = 3;   // uint4 per slot
+// An IPv4 slot is one uint4 (UPE_TSS_SLOT16, the default): the masked key's free bits carry the
+// rest — k0's low byte (the IP version, never part of a group's mask) and k1's high half (above
+// the 16-bit destination port) hold v = (index + 1) | action << 22 (0 = empty slot), so a probe
+// is one 16-byte load, one memory request (two loads into one line were two requests:
+// tools/fetch_calib), and the IPv4 slot array takes half the L2.
+#ifndef UPE_TSS_SLOT16
+#define UPE_TSS_SLOT16 1
+#endif
+constexpr bool kTssSlot16 = UPE_TSS_SLOT16;
+constexpr int kTssSlot4 = kTssSlot16 ? 1 : 2, kTssSlot6 = 3;   // uint4 per slot
+constexpr uint32_t kTssMaxRules = 1u << 22;   // index + 1 in 22 bits, the action above it
 // Fingerprints of small groups staged in LDS (word [15] of such a group: 1 + its offset in the
 // staged image): their probes then wait for no fingerprint round trip.
 #ifndef UPE_FP_STAGE_MAX
@@ -427,6 +437,23 @@ __device__ __forceinline__ uint32_t csum_fold(unsigned long long sum) {
     return (~f) & 0xFFFFu;
 }
 __device__ __forceinline__ void store16(uint4* p, uint4 v) { *p = v; }
+// Frame-window and descriptor loads (diagnostic UPE_LOAD_NT: bit 0 frames, bit 1 descriptors as
+// non-temporal loads: read once, streamed).
+#ifndef UPE_LOAD_NT
+#define UPE_LOAD_NT 0
+#endif
+__device__ __forceinline__ uint4 ldf(const uint4* p) {
+    if (UPE_LOAD_NT & 1) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+        return make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return *p;
+}
+__device__ __forceinline__ uint64_t ldd(const uint64_t* p) {
+    if (UPE_LOAD_NT & 2) return __builtin_nontemporal_load(p);
+    return *p;
+}
 // The in-place header stores (diagnostic UPE_FRAME_SC1: written through, lines dropped from L2).
 __device__ __forceinline__ void store16_frame(uint4* p, uint4 v) {
 #if UPE_FRAME_SC1
@@ -715,7 +742,7 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
     const auto* G6 = as_const<u32x16>(a.tg6);
     const uint16_t* FP = is6 ? a.tf6 : a.tf4;
     const uint4* T = is6 ? a.tt6 : a.tt4;
-    const uint32_t st = is6 ? 3u : 2u;   // slot stride in uint4
+    const uint32_t st = is6 ? (uint32_t)kTssSlot6 : (uint32_t)kTssSlot4;   // slot stride in uint4
     for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t gu = __builtin_amdgcn_readfirstlane(g);
         u32x16 q4 = {}, q6 = {};
@@ -776,17 +803,22 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
             const bool m1 = f1 == tag, m2 = f2 == tag;
             uint32_t idx = kNone, ac = 0;
             auto probe = [&](uint32_t t) {
-                const uint4 A = T[st * t], B = T[st * t + 1];
-                uint4 C = make_uint4(0, 0, 0, 0);
+                const uint4 A = T[st * t];
+                uint4 B = make_uint4(0, 0, 0, 0), C = B;
+                if (is6 || !kTssSlot16) B = T[st * t + 1];
                 if (is6) C = T[st * t + 2];
                 const bool k4 = A.x == kw[0] && A.y == kw[1] && A.z == kw[2] && A.w == kw[3];
+                // the compact IPv4 slot: v = (index + 1) | action << 22 in the key's free bits
+                const uint32_t v = (A.x & 0xFFu) | ((A.y >> 16) << 8);
+                const bool k4c = (A.x & ~0xFFu) == kw[0] && (A.y & 0xFFFFu) == kw[1] &&
+                                 A.z == kw[2] && A.w == kw[3];
                 const bool hit = is6 ? ((C.w & 1u) && k4 && B.x == kw[4] && B.y == kw[5] &&
                                         B.z == kw[6] && B.w == kw[7] && C.x == kw[8] &&
                                         C.y == kw[9])
-                                     : (B.y != 0u && k4);
+                                     : kTssSlot16 ? (v != 0u && k4c) : (B.y != 0u && k4);
                 if (hit) {
-                    idx = is6 ? C.z : B.x;
-                    ac = is6 ? (C.w >> 8) : B.z;
+                    idx = is6 ? C.z : kTssSlot16 ? (v & (kTssMaxRules - 1u)) - 1u : B.x;
+                    ac = is6 ? (C.w >> 8) : kTssSlot16 ? v >> 22 : B.z;
                 }
                 return hit;
             };
@@ -1158,7 +1190,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
                 if (c < 3 || len > 16u * c) {
-                    const uint4 v = q[c];
+                    const uint4 v = ldf(&q[c]);
                     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
                 }
             }
@@ -1177,10 +1209,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            v.c0 = q[0]; v.c1 = q[1]; v.c2 = q[2];
+            v.c0 = ldf(&q[0]); v.c1 = ldf(&q[1]); v.c2 = ldf(&q[2]);
             if (!kWin48) {
-                if (len > 48u) v.c3 = q[3];
-                if (len > 64u) v.c4 = q[4];
+                if (len > 48u) v.c3 = ldf(&q[3]);
+                if (len > 64u) v.c4 = ldf(&q[4]);
             }
         }
         return v;
@@ -1219,7 +1251,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // rule tables into LDS, before the entry barrier.  (Issuing the first chunk's window loads
     // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
     uint64_t dsc_next = 0;
-    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[ch * 64u + lane];
+    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[ch * 64u + lane]);
     if (!kTssMode && small_stats) {
         const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
         const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
@@ -1354,7 +1386,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
         have_nw = false;
         dsc_next = 0;
-        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
+        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[chn * 64u + lane]);
         if (!folded) fold_start();
 
         if (first) STAMP_VM(2);
@@ -1660,7 +1692,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (late) {
             chn = claim();
             dsc_next = 0;
-            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
+            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[chn * 64u + lane]);
             asm volatile("" : "+v"(dsc_next));   // consumed here (see before the loop)
         }
     }
@@ -2755,7 +2787,10 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
             out.fp[fbase + t] = tss_tag(tss_hash(k.data(), nw, seed));
             uint4* e = &out.slots[base + t * per];
             const uint32_t act = act_code(rules[idx[slot[t]]].action.type);
-            if (F == 4) {
+            if (F == 4 && kTssSlot16) {
+                const uint32_t v = (idx[slot[t]] + 1u) | act << 22;
+                e[0] = make_uint4(k[0] | (v & 0xFFu), k[1] | ((v >> 8) << 16), k[2], k[3]);
+            } else if (F == 4) {
                 e[0] = make_uint4(k[0], k[1], k[2], k[3]);
                 e[1] = make_uint4(idx[slot[t]], 1u, act, 0u);
             } else {
@@ -2868,7 +2903,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     c->nfs = 0;
     c->ng4 = c->ng6 = 0;
     const char* force = getenv("UPE_GPU_TSS");   // diagnostic: 0 = never, 1 = always
-    if (count > 0 && !(force && force[0] == '0')) {
+    if (count > 0 && count < kTssMaxRules && !(force && force[0] == '0')) {
         TssFamily f4, f6;
         if (build_tss_family(4, v4, v6, rules, count, f4) &&
             build_tss_family(6, v4, v6, rules, count, f6)) {
