@@ -320,6 +320,59 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                     "cycled, same timing protocol as value (barrier, max over ranks)"}
 
 
+def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
+    """Ring mode (upe_gpu_process_ring_emit, not `value`): `count` batches of this workload, each
+    its own copy of the frames, laid out back to back and classified by ONE launch; the launch's
+    fixed cost is paid once per ring.  Reports the per-batch rate and each batch's completion
+    time within the launch (the device stamps of the last ring)."""
+    from upe_amd import shard
+
+    n = wl.n
+    fbytes = int(wl.frames.nbytes)
+    stride = (fbytes + 255) // 256 * 256
+    pristine = torch.from_numpy(wl.frames).to(dev)
+    frames = torch.empty(count * stride, dtype=torch.uint8, device=dev)
+    for k in range(count):
+        frames[k * stride: k * stride + fbytes].copy_(pristine)
+    del pristine
+    d0 = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    desc = torch.cat([d0 + ((k * stride) << 16) for k in range(count)])
+    verdict = torch.empty(n * count, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n * count * 16, dtype=torch.uint8, device=dev)
+    done = torch.zeros(count, dtype=torch.int64, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+
+    def run(k: int) -> None:
+        for _ in range(k):
+            worker.process_ring_emit(frames, desc, verdict, hdr, n, count, done, sh)
+
+    run(2)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    run(launches)
+    ev[1].record()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    total = float(shard.sum_over_ranks([n * count * launches], dist, dev)[0])
+    ring_us = ev[0].elapsed_time(ev[1]) * 1e3 / launches
+    stamps = (done.cpu().numpy() / 1e3).round(2).tolist()   # us after the launch's start
+    del frames, desc, verdict, hdr, done
+    return {"value": round(total / elapsed / 1e6, 2), "unit": "Mpps", "batches_per_launch": count,
+            "packets_per_batch": n, "launches": launches,
+            "us_per_launch": round(ring_us, 2), "us_per_batch": round(ring_us / count, 3),
+            "batch_done_us": stamps,
+            "what": "upe_gpu_process_ring_emit: the batches of a ring (each its own frames copy) "
+                    "in ONE launch, emit mode; batch_done_us = each batch's completion (its last "
+                    "stores issued) after the launch's first workgroup started, device clock; "
+                    "not value (value = one launch per batch)"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -357,6 +410,8 @@ def main() -> None:
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
     ap.add_argument("--imix-copies", type=int, default=32)
+    ap.add_argument("--ring", type=int, default=16,
+                    help="batches per launch of the ring leg (config B; 0 skips it)")
     args = ap.parse_args()
 
     import torch
@@ -501,6 +556,9 @@ def main() -> None:
     if args.config == "B" and not args.no_imix and not args.packets:
         imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
                         args.imix_copies)
+    ring = None
+    if args.config == "B" and args.ring > 0 and not args.packets:
+        ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
     probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
@@ -588,6 +646,8 @@ def main() -> None:
             out["other_mode"] = other
         if imix:
             out["imix"] = imix
+        if ring:
+            out["ring"] = ring
         if shared:
             out["workers_sharing_gpu"] = shared
         def host_line(h, what):

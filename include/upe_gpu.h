@@ -256,6 +256,22 @@ typedef struct {
 int upe_gpu_process_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                          uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n, void *stream);
 
+/* A ring of `count` resident batches of n packets each in ONE launch (throughput mode): the
+ * batches lie back to back in the "Batch layout" (batch j = descriptors, verdicts and records
+ * [j*n, (j+1)*n), frames anywhere in d_frames) and are classified in ring order by one
+ * persistent launch in emit mode, so the per-launch cost (dispatch, the first windows' round
+ * trip, the tail, the boundary) is paid once per ring, not once per batch.  Counters,
+ * rule_stats, the L1 state, every verdict code and every record equal those of `count`
+ * back-to-back upe_gpu_process_emit() calls over the batches; UPE_VF_L1_INIT is relative to the
+ * ring's start.  n a multiple of 1024, n * count <= 2^24.  d_done_ns (optional, device or
+ * host-mapped, count entries): for each batch, the time (ns) from the launch's first workgroup
+ * to the moment its last workgroup had issued the batch's last stores — per-batch completion
+ * latency — or 0 where not stamped (stamps need a linear-scan table and batches of at least
+ * one tile per persistent workgroup, 256k packets on MI355X).  Asynchronous on `stream`. */
+int upe_gpu_process_ring_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                              uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n, size_t count,
+                              uint64_t *d_done_ns, void *stream);
+
 /* Apply one record to its frame (host; src/worker.c:174-176,197-200,213,227-230 as bytes). */
 void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec);
 

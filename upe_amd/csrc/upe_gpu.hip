@@ -345,6 +345,13 @@ struct Args {
     unsigned long long launch_tag;   // this launch's index + 1
     uint32_t* defer;                 // deferred look-back candidates: index | family << 31
     uint32_t lb_spin;                // longest look-back wait, 100 MHz ticks (then defer)
+    // ring launch (upe_gpu_process_ring_emit): batches of ring_cpb chunks each; per batch the
+    // workgroups that have finished it, and the clock (10 ns) at which the last one did,
+    // relative to the first workgroup's start (ring_t0)
+    uint32_t ring_cpb, ring_mine;    // chunks per batch, and per batch and workgroup
+    uint32_t* ring_wg;
+    unsigned long long* ring_done;
+    unsigned long long* ring_t0;
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
@@ -1151,7 +1158,9 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // the tables (agreement then holds until the host changes the tables or the L1 state) or whose
 // family's index is empty; the look-back is not compiled in, and an entry that disagrees with an
 // empty index answers its candidates itself (no packet can hit that table first).
-template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false>
+// kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
+// workgroup owning part of it has finished its chunks of it; the last one stamps the time.
+template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1161,6 +1170,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
+    __shared__ uint32_t s_bdone[kRing ? 4 : 1];   // ring: chunks finished per batch (4 in flight)
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -1244,6 +1254,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         return t < a.ntiles && c * 64u < a.n ? c : kNone;
     };
     if (tid == 0) s_claim = kWaves;
+    if (kRing && tid < 4) s_bdone[tid] = 0u;
+    if (kRing && tid == 0)   // the ring's time origin: the first workgroup to start
+        __hip_atomic_fetch_min(a.ring_t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < C_N + 3) s_tot[tid] = tid < C_N ? 0u : kNone;
     if (tid < 2 * kWaves) s_wm[tid / 2][tid % 2] = 0u;
     uint32_t ch = chunk_of((uint32_t)wave);   // this wave's chunk
@@ -1685,6 +1699,29 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (h6 && lane == 63 - __builtin_clzll(h6)) {
                 s_pay[wave][3] = r.d[0]; s_pay[wave][4] = r.d[1]; s_pay[wave][5] = r.d[2];
                 s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
+            }
+        }
+        if (kRing) {
+            // every workgroup owns ring_mine chunks of each batch (the host launches the ring
+            // kernel only when a batch's tiles divide evenly over the grid)
+            const uint32_t j = ch / a.ring_cpb, mine = a.ring_mine;
+            uint32_t d = 0;
+            if (lane == 0) d = atomicAdd(&s_bdone[j & 3u], 1u) + 1u;
+            d = __builtin_amdgcn_readfirstlane(d);
+            if (d == mine) {   // the workgroup is done with batch j
+                uint32_t t = 0;
+                if (lane == 0) {
+                    s_bdone[j & 3u] = 0u;
+                    t = atomicAdd(&a.ring_wg[j], 1u) + 1u;
+                }
+                t = __builtin_amdgcn_readfirstlane(t);
+                if (lane == 0 && t == gridDim.x) {
+                    const unsigned long long t0 = __hip_atomic_load(a.ring_t0, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&a.ring_done[j],
+                                       ((unsigned long long)__builtin_amdgcn_s_memrealtime() - t0) * 10ull,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
         if (kMid && kWin48 == 2 && have_nw)
@@ -2169,6 +2206,8 @@ struct upe_gpu_ctx {
     bool allow_nolb = true;        // UPE_GPU_NOLB=0: never use the kernels without look-back
     int last_var = -1;             // kernel variant of the last classify launch
     uint32_t last_grid = 0;
+    unsigned long long* ring_wg = nullptr;   // ring launches: per-batch counters + time origin
+    size_t ring_alloc = 0;
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
@@ -2362,22 +2401,25 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-// Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only).
-constexpr int kVarCount = 16;
-int classify_var(bool tss, bool emit, bool lean, bool nolb) {
-    return (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+constexpr int kVarCount = 32;
+// Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
+// bit 4 ring (lean emit linear scan only).
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false) {
+    return (ring ? 16 : 0) | (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
 }
 template <int V>
 const void* classify_fn_of() {
     return reinterpret_cast<const void*>(
-        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0>);
+        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0>);
 }
 const void* classify_fn(int var) {
     static const void* const fns[kVarCount] = {
         classify_fn_of<0>(), classify_fn_of<1>(), classify_fn_of<2>(), classify_fn_of<3>(),
         classify_fn_of<4>(), classify_fn_of<5>(), classify_fn_of<6>(), classify_fn_of<7>(),
         nullptr, nullptr, nullptr, nullptr,
-        classify_fn_of<12>(), classify_fn_of<13>(), classify_fn_of<14>(), classify_fn_of<15>()};
+        classify_fn_of<12>(), classify_fn_of<13>(), classify_fn_of<14>(), classify_fn_of<15>(),
+        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<21>(), nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<29>(), nullptr, nullptr};
     return var >= 0 && var < kVarCount ? fns[var] : nullptr;
 }
 
@@ -2400,8 +2442,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
 // launch the first time the configuration is used (census_probe).  0 on error.
 uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
-    static_assert(kVarCount <= 16, "the variant takes the key's low 4 bits");
-    const uint64_t key = (uint64_t)lds << 4 | (uint64_t)var;
+    static_assert(kVarCount <= 32, "the variant takes the key's low 5 bits");
+    const uint64_t key = (uint64_t)lds << 5 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
     int per_cu = 0;
@@ -2631,6 +2673,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->defer) (void)hipFree(c->defer);
+    if (c->ring_wg) (void)hipFree(c->ring_wg);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     for (auto& sl : c->hs) {
@@ -3082,13 +3125,20 @@ namespace {
 // packets (the kernel's per-lane counters are 16-bit halves; a lane sees at most one packet
 // per tile).
 constexpr size_t kMaxLaunch = (size_t)1 << 24;
+// A ring launch's completion stamps (upe_gpu_process_ring_emit): batches of `per` packets.
+struct RingReq {
+    size_t per;
+    unsigned long long* done;   // [count] ns after the first workgroup's start, 0 = not stamped
+};
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
-                 uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
+                 uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
+                 const RingReq* ring = nullptr) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
     if (((uintptr_t)d_frames & 15u) != 0) return fail("frames buffer must be 16-byte aligned");
     if (((uintptr_t)d_hdr & 15u) != 0) return fail("header records must be 16-byte aligned");
+    if (ring && n > kMaxLaunch) return fail("a ring holds at most 2^24 packets");
     if (n > kMaxLaunch) {
         // consecutive launches of at most kMaxLaunch packets: the worker's stream semantics are
         // those of one batch (batch_info describes the last launch)
@@ -3212,13 +3262,16 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     }
     a.agree_out = c->no_lb ? nullptr : c->agree_d;
     a.launch_tag = c->k + 1;
-    const int var = classify_var(c->tss, emit, lean, c->no_lb);
+    // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
+    bool stamp = ring && ring->done && emit && lean && !c->tss;
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
-    const uint32_t grid_cap = resident_grid(c, var, lds, s);
+    uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
-    if (lean && !c->no_lb && resident_grid(c, classify_var(c->tss, emit, true, true), lds, s) == 0)
+    if (lean && !c->no_lb &&
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3229,6 +3282,33 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.tw = tw;
     a.ntiles = (nchunks + tw - 1) / tw;
     const uint32_t grid = a.ntiles == 0 ? 1u : a.ntiles < grid_cap ? a.ntiles : grid_cap;
+    if (ring && ring->done) {
+        HIP_TRY(hipMemsetAsync(ring->done, 0, (n / ring->per) * sizeof(unsigned long long), s));
+        // every workgroup must own the same number of tiles of every batch (at least one), so
+        // that it has at most two batches in flight (kRing's four LDS counters)
+        const size_t tpb = (ring->per / 64) / tw;
+        if (stamp && (tpb < grid || tpb % grid != 0)) stamp = false;
+        if (!stamp) {
+            var = classify_var(c->tss, emit, lean, c->no_lb, false);
+            if (resident_grid(c, var, lds, s) == 0) return -1;
+        } else {
+            const size_t nb = n / ring->per;
+            if (nb > c->ring_alloc) {
+                if (c->ring_wg) HIP_TRY(hipFree(c->ring_wg));
+                c->ring_wg = nullptr;
+                c->ring_alloc = 0;
+                HIP_TRY(hipMalloc(&c->ring_wg, (nb + 2) * sizeof(unsigned long long)));
+                c->ring_alloc = nb;
+            }
+            HIP_TRY(hipMemsetAsync(c->ring_wg, 0, nb * sizeof(unsigned long long), s));
+            HIP_TRY(hipMemsetAsync(c->ring_wg + nb, 0xFF, sizeof(unsigned long long), s));
+            a.ring_cpb = (uint32_t)(ring->per / 64);
+            a.ring_mine = (uint32_t)(tpb / grid * tw);
+            a.ring_wg = reinterpret_cast<uint32_t*>(c->ring_wg);
+            a.ring_done = ring->done;
+            a.ring_t0 = c->ring_wg + nb;
+        }
+    }
     launch_classify(var, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
     c->last_var = var;
@@ -3292,6 +3372,18 @@ int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_
                          uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (n && !d_hdr) return fail("null header records");
     return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
+}
+
+int upe_gpu_process_ring_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                              uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, size_t count,
+                              uint64_t* d_done_ns, void* stream) {
+    if (!c) return fail("null context");
+    if (count == 0 || n == 0) return 0;
+    if (!d_hdr) return fail("null header records");
+    if (n % 1024 != 0) return fail("a ring batch must hold a multiple of 1024 packets");
+    if (n * count > kMaxLaunch) return fail("a ring holds at most 2^24 packets");
+    const RingReq r{n, reinterpret_cast<unsigned long long*>(d_done_ns)};
+    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n * count, stream, &r);
 }
 
 }  // extern "C"

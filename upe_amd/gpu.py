@@ -70,6 +70,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_segmented": (I, [P, P, P, P, SZ, P, SZ, P, SZ, ctypes.c_int64, P, P]),
         "upe_gpu_process_emit": (I, [P, P, P, P, P, SZ, P]),
         "upe_gpu_process_batches_emit": (I, [P, P, P, P, P, SZ, SZ, P]),
+        "upe_gpu_process_ring_emit": (I, [P, P, P, P, P, SZ, SZ, P, P]),
         "upe_hdr_apply": (None, [P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
@@ -103,6 +104,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_gpu_process_host_emit",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
             "upe_gpu_process_segmented", "upe_gpu_process_emit", "upe_gpu_process_batches_emit",
+            "upe_gpu_process_ring_emit",
             "upe_hdr_apply",
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
@@ -245,6 +247,15 @@ class GpuWorker:
                                                 _dev_ptr(hdr), n, len(frames_ptrs),
                                                 stream or None),
                "upe_gpu_process_batches_emit")
+
+    def process_ring_emit(self, frames, desc, verdict, hdr, n: int, count: int, done_ns=None,
+                          stream=None) -> None:
+        """upe_gpu_process_ring_emit: `count` batches of n packets laid out back to back, one
+        launch; done_ns (device uint64[count] or None) receives per-batch completion times."""
+        _check(LIB.upe_gpu_process_ring_emit(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
+                                             _dev_ptr(verdict), _dev_ptr(hdr), n, count,
+                                             _dev_ptr(done_ns) or None, stream or None),
+               "upe_gpu_process_ring_emit")
 
     def process_batches(self, frames_ptrs, desc, verdict, n: int, stream=None) -> None:
         """Queue len(frames_ptrs) batches (device pointers) back to back from native code."""
