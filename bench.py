@@ -350,17 +350,15 @@ def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
-    ev[0].record()
     run(launches)
-    ev[1].record()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
     total = float(shard.sum_over_ranks([n * count * launches], dist, dev)[0])
-    ring_us = ev[0].elapsed_time(ev[1]) * 1e3 / launches
+    # (wall time: the launches go to the worker's own stream when torch's is the null stream)
+    ring_us = elapsed * 1e6 / launches
     stamps = (done.cpu().numpy() / 1e3).round(2).tolist()   # us after the launch's start
     del frames, desc, verdict, hdr, done
     return {"value": round(total / elapsed / 1e6, 2), "unit": "Mpps", "batches_per_launch": count,

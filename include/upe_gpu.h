@@ -319,10 +319,36 @@ int upe_gpu_host_free(void *ptr);
 int upe_gpu_process_batches(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
                             const uint64_t *d_desc, uint32_t *d_verdict, size_t n, size_t count,
                             void *stream);
-/* The same in emit mode (every batch writes its records to d_hdr). */
+/* The same in emit mode (every batch writes its records to d_hdr): upe_gpu_process_queue_emit()
+ * over `count` batches that share d_desc, d_verdict and d_hdr. */
 int upe_gpu_process_batches_emit(upe_gpu_ctx_t *ctx, uint8_t *const *d_frames_list,
                                  const uint64_t *d_desc, uint32_t *d_verdict,
                                  upe_hdr_rec_t *d_hdr, size_t n, size_t count, void *stream);
+
+/* One resident batch of a queue: device frames, descriptors, verdicts and records, n packets. */
+typedef struct upe_gpu_batch {
+    uint8_t *frames;
+    const uint64_t *desc;
+    uint32_t *verdict;
+    upe_hdr_rec_t *hdr;
+    size_t n;
+} upe_gpu_batch_t;
+
+/* The worker loop (reference src/worker.c:255-307: burst after burst, the worker's state carried
+ * from one to the next) over `count` resident batches in emit mode, one launch per batch, with
+ * consecutive launches overlapped: launch k + 1 goes to a second stream and is dispatched once
+ * every workgroup of launch k is resident (a stream wait on a signal word launch k's last
+ * workgroup to start writes), so its workgroups take CUs as launch k's finish, stage their
+ * tables and then wait inside the kernel for launch k's finished-workgroup count before they
+ * read the state it leaves.  The kernel-boundary gap and the next batch's prologue are hidden
+ * behind the previous batch's tail.  Results — every verdict, record, counter, rule_stats word
+ * and the L1 state — equal `count` upe_gpu_process_emit() calls in order; batches may share
+ * descriptor and output buffers (each batch's stores come after the previous batch's finished).
+ * Falls back to sequential launches for tables of more than 4096 rules (their rule_stats
+ * group-by follows each launch), batches over 2^24 packets, or UPE_GPU_OVERLAP=0.  `stream`
+ * orders the queue after earlier work and everything after it.  0 / -1. */
+int upe_gpu_process_queue_emit(upe_gpu_ctx_t *ctx, const upe_gpu_batch_t *batches, size_t count,
+                               void *stream);
 
 /* upe_gpu_process() plus software RSS in the same pass (reference src/rx_pcap.c:67-77 parses
  * every packet a second time on the RX thread for this): d_flow_hash[i] (device, n uint32) =
@@ -373,7 +399,8 @@ typedef struct {
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */
-    uint32_t reserved;
+    uint32_t overlapped; /* launches so far that ran overlapped with their predecessor
+                            (upe_gpu_process_queue_emit) */
     uint64_t launches; /* classify launches of this context so far */
 } upe_launch_info_t;
 int upe_gpu_launch_info(upe_gpu_ctx_t *ctx, upe_launch_info_t *info);
@@ -441,6 +468,7 @@ const char *upe_host_last_error(void);
 #else
 #define UPE_STATIC_ASSERT _Static_assert
 #endif
+UPE_STATIC_ASSERT(sizeof(upe_gpu_batch_t) == 40, "upe_gpu_batch_t layout");
 UPE_STATIC_ASSERT(sizeof(upe_flow_key_t) == 44, "flow_key_t layout");
 UPE_STATIC_ASSERT(offsetof(upe_flow_key_t, dst_ip) == 20, "flow_key_t.dst_ip");
 UPE_STATIC_ASSERT(offsetof(upe_flow_key_t, protocol) == 40, "flow_key_t.protocol");

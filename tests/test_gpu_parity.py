@@ -287,11 +287,19 @@ def test_full_size_digest(gpu_worker_factory, key, make, emit):
     assert _sha(l1) == dg["l1"]
 
 
-def test_config_d_full_properties(gpu_worker_factory):
+_D_CACHE: dict = {}
+
+
+@pytest.mark.parametrize("emit", [False, True])
+def test_config_d_full_properties(gpu_worker_factory, emit):
     """16M packets x 64k rules: size-independent checks (counter identities, stats sums,
-    parse-fail and TTL invariants) plus random 4k-packet chunks against the oracle."""
+    parse-fail and TTL invariants), the first 64k packets (from the calloc'd L1 state the batch
+    starts with) exactly — every verdict bit and every output byte, rewritten in place or
+    through the records — and random 4k-packet chunks against the oracle."""
+    from upe_amd.layout import desc_lens, desc_offsets
+
     wl = synth.config_d()
-    frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl)
+    frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl, emit=emit)
     c = counters[0]
     codes = np.bincount(verdict & 0xF, minlength=7)
     assert int(c["pkts_in"]) == wl.n
@@ -299,8 +307,19 @@ def test_config_d_full_properties(gpu_worker_factory):
     assert int(c["pkts_dropped"]) + int(c["pkts_forwarded"]) + int(c["pkts_consumed"]) == wl.n
     assert int(stats["packets"].sum()) == int(c["pkts_matched"])
     assert int(c["pkts_parsed"]) == int(c["pkts_matched"])  # catch-all rule
-    rng = np.random.default_rng(7)
     rs = wl.rules_sorted
+    pre = wl.copy()
+    pre.desc = wl.desc[:1 << 16]
+    if "d_prefix" not in _D_CACHE:   # ~20 s of oracle work, shared by both modes
+        _D_CACHE["d_prefix"] = oracle.run_restated(pre, rules_sorted=rs)
+    r = _D_CACHE["d_prefix"]
+    bad = np.nonzero(verdict[:1 << 16] != r.verdict)[0]
+    assert bad.size == 0, f"prefix verdicts differ at {bad[:8].tolist()}"
+    offs, lens = desc_offsets(pre.desc).astype(np.int64), desc_lens(pre.desc).astype(np.int64)
+    mine = np.repeat(offs, lens) + (np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens))
+    assert np.array_equal(frames[mine], r.frames[mine]), "prefix output bytes differ"
+    assert not np.array_equal(frames[mine], wl.frames[mine])   # the prefix forwards packets
+    rng = np.random.default_rng(7)
     for start in rng.integers(0, wl.n - 4096, size=4):
         sub = wl.copy()
         sub.desc = wl.desc[start:start + 4096]

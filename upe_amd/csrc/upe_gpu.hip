@@ -210,11 +210,13 @@ struct __attribute__((aligned(128))) BatchAcc {
     uint32_t ctrl[kReps];                  // kNone - first control packet (max)
     uint32_t grid;                         // the batch's grid
     uint32_t n;                            // the batch's size
+    uint32_t pad0[30];
     // look-back give-ups (a launch that started from a disagreeing L1 entry): workgroups that have
     // finished, deferred (chunk, family) entries, and "some wave gave up" (later waves then wait
-    // for no unpublished flag at all)
+    // for no unpublished flag at all).  A line of their own: the batch's launch polls them
+    // while an overlapped next launch may read grid and n.
     uint32_t done, ndefer, giveup;
-    uint32_t pad[27];
+    uint32_t pad[29];
 };
 // Payload of a workgroup's last table hit per family; the next batch reads the one the batch
 // maximum points at.
@@ -233,11 +235,21 @@ constexpr uint32_t kLbTagMod = 0x3FFFFFFu;   // tags 1 .. kLbTagMod
 
 // Everything a batch reads or writes besides the packets and the tables, in one device
 // allocation.
+// One L1 state slot per 128-byte line: overlapped launches (upe_gpu_process_queue_emit) read one
+// slot while the other is written, and a line another XCD's L2 holds must not carry both.
+struct __attribute__((aligned(128))) L1Slot {
+    DevL1 s;
+};
 struct DevState {
-    DevL1 l1[2];
+    L1Slot l1[2];
     BatchAcc acc[3];
     unsigned long long totals[8];                           // cumulative, upe_counters_t order
-    uint32_t pad0[16];
+    // overlapped launches (upe_gpu_process_queue_emit): workgroups of counting launches finished
+    // and started (cumulative; Args::fin_flags)
+    uint32_t fin;
+    uint32_t pad0[31];
+    uint32_t started;
+    uint32_t pad1[31];
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
     uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
@@ -352,10 +364,19 @@ struct Args {
     uint32_t* ring_wg;
     unsigned long long* ring_done;
     unsigned long long* ring_t0;
+    // overlapped launches (upe_gpu_process_queue_emit): bit 0 this launch counts its finished
+    // workgroups into st->fin once every wave's stores have drained; bit 1 its workgroups wait,
+    // after the table staging, until st->fin reaches fin_wait (the previous launch, on another
+    // stream, has finished); bit 2 its workgroups count themselves started into st->started,
+    // and the one that brings it to start_target stores launch_tag into the signal word `sig`
+    // (the next launch's stream waits for that before it dispatches: every workgroup of this
+    // launch is resident before any of the next, so the next one's wait always ends)
+    uint32_t fin_flags, fin_wait, start_target;
+    unsigned long long* sig;
 };
 // Batch k's state slots, from Args (DevState comment).
-__device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2]; }
-__device__ __forceinline__ DevL1* l1_out(const Args& a) { return &a.st->l1[(a.k6 + 1) % 2]; }
+__device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2].s; }
+__device__ __forceinline__ DevL1* l1_out(const Args& a) { return &a.st->l1[(a.k6 + 1) % 2].s; }
 __device__ __forceinline__ BatchAcc* acc_cur(const Args& a) { return &a.st->acc[a.k6 % 3]; }
 __device__ __forceinline__ const BatchAcc* acc_prev(const Args& a) { return &a.st->acc[(a.k6 + 2) % 3]; }
 __device__ __forceinline__ BatchAcc* acc_next(const Args& a) { return &a.st->acc[(a.k6 + 1) % 3]; }
@@ -588,6 +609,13 @@ __global__ void upe_refresh(DevL1* l1, NeighIndex arp, NeighIndex ndp) {
 // (s_load) loads, which it will not do through a generic pointer it cannot prove unwritten.
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// A write-through (sc1) store: the line leaves this XCD's L2, so a reader on another XCD that
+// has not cached it sees the value once the storing wave's stores have drained.
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename V, typename T>
 __device__ __forceinline__ const __attribute__((address_space(4))) V* as_const(const T* p) {
     return (const __attribute__((address_space(4))) V*)p;
@@ -1160,7 +1188,8 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // empty index answers its candidates itself (no packet can hit that table first).
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
-template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false>
+template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
+          bool kQueue = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1171,6 +1200,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
     __shared__ uint32_t s_bdone[kRing ? 4 : 1];   // ring: chunks finished per batch (4 in flight)
+    __shared__ uint32_t s_fin;     // queue launches: waves finished (fin_flags bit 0)
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -1254,6 +1284,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         return t < a.ntiles && c * 64u < a.n ? c : kNone;
     };
     if (tid == 0) s_claim = kWaves;
+    if (kQueue && tid == 0) s_fin = 0u;
     if (kRing && tid < 4) s_bdone[tid] = 0u;
     if (kRing && tid == 0)   // the ring's time origin: the first workgroup to start
         __hip_atomic_fetch_min(a.ring_t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
@@ -1278,10 +1309,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // outcome folded in (its replicated minima / maxima, then at most two payload loads).
     // DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4], ndp_mac_lo/hi, arp_ok, ndp_ok.
     static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
-    const u32x16 lin = *as_const<u32x16>(l1_in(a));
+    // (A queue launch loads them once the previous launch has finished: below.)
+    u32x16 lin;
     unsigned long long pr[R_N] = {0, 0, 0, 0};
-    if (lane < kReps)
-        for (int j = 0; j < R_N; ++j) pr[j] = acc_prev(a)->l1r[lane][j];
+    const bool q_wait = kQueue && (a.fin_flags & 2u);   // a queue launch after the first
+    auto load_prev = [&]() {
+        lin = *as_const<u32x16>(l1_in(a));
+        if (lane < kReps)
+            for (int j = 0; j < R_N; ++j)
+                pr[j] = kQueue ? __hip_atomic_load(&acc_prev(a)->l1r[lane][j], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : acc_prev(a)->l1r[lane][j];
+    };
+    if (!kQueue) load_prev();
     // small neighbour indexes into LDS after the rule-stats bins: a lookup is then an LDS read,
     // not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
@@ -1309,28 +1349,46 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if ((uint32_t)j % gridDim.x != blockIdx.x) continue;
-                const uint32_t v = j == 0 ? *as_const<uint32_t>(&acc_prev(a)->n)
-                                          : wave_reduce<0>(lane < kReps ? acc_prev(a)->cnt[lane][j - 1]
-                                                                        : 0u);
-                if (lane == 0 && v) a.st->totals[j] += v;
+                const uint32_t v =
+                    j == 0 ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                 &acc_prev(a)->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                           : wave_reduce<0>(lane < kReps ? __hip_atomic_load(&acc_prev(a)->cnt[lane][j - 1],
+                                                                             __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT)
+                                                         : 0u);
+                if (lane == 0 && v) atomicAdd(&a.st->totals[j], (unsigned long long)v);
             }
         }
         if (blockIdx.x == 0) {
             // workgroup 0: this batch's grid and size, batch k + 1's accumulators re-armed
             // (batch k - 2's, folded by batch k - 1)
+            // (written through: an overlapped next launch reads them from another XCD)
             if (lane == 0) {
-                acc_cur(a)->grid = gridDim.x;
-                acc_cur(a)->n = a.n;
+                st_wt(&acc_cur(a)->grid, gridDim.x);
+                st_wt(&acc_cur(a)->n, a.n);
             }
             uint32_t* nc = &acc_next(a)->cnt[0][0];
             unsigned long long* nr = &acc_next(a)->l1r[0][0];
-            for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) nc[k] = 0u;
-            for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) nr[k] = 0ull;
-            if (lane < kReps) acc_next(a)->ctrl[lane] = 0u;
-            if (lane < 3) (&acc_next(a)->done)[lane] = 0u;   // done, ndefer, giveup
+            for (uint32_t k = lane; k < (uint32_t)(kReps * C_N); k += 64) st_wt(&nc[k], 0u);
+            for (uint32_t k = lane; k < (uint32_t)(kReps * R_N); k += 64) st_wt(&nr[k], 0ull);
+            if (lane < kReps) st_wt(&acc_next(a)->ctrl[lane], 0u);
+            if (lane < 3) st_wt(&(&acc_next(a)->done)[lane], 0u);   // done, ndefer, giveup
         }
     };
     auto fold_start = [&]() {
+        if (q_wait) {
+            // The previous launch runs on another stream and may not have finished (this wave's
+            // first window loads are in flight meanwhile): wait for its finished-workgroup count
+            // (every workgroup of it is resident: fin_flags bit 2).  Everything this launch reads
+            // of the previous one's (L1 state, accumulators, payloads) was stored write-through
+            // or by atomics and drained before that count, on lines nothing here has touched
+            // since this launch began.
+            while ((int32_t)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                 &a.st->fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
+                             a.fin_wait) < 0)
+                __builtin_amdgcn_s_sleep(2);
+            load_prev();
+        }
         if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
 #pragma unroll
             for (int j = 0; j < 11; ++j) L1[j] = lin[j];
@@ -1342,7 +1400,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
         folded = true;
     };
-    if (wave == 0 && blockIdx.x < 8) books();
+    // A queue launch counts its workgroups started (after the staging, so that the atomic's
+    // round trip is not in front of the staging loads): the one that completes the count stores
+    // the launch tag into the signal word the next launch's stream waits on.
+    if (kQueue && (a.fin_flags & 4u) && tid == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(&a.st->started, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (t + 1u == a.start_target)
+            __hip_atomic_store(a.sig, a.launch_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (kQueue && !q_wait) load_prev();
+    if (!q_wait && wave == 0 && blockIdx.x < 8) books();
 
     // Persistent workgroups: the grid is what the chip holds at once, so the per-workgroup
     // flush happens once per workgroup, at the very end of its life.  (Per-wave claims from
@@ -1776,8 +1844,25 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (v) atomicAdd(&rep[k], (unsigned long long)v);
         }
     }
-    if (wave != 0) return;
+    // overlapped launches: the last wave of the workgroup to drain its stores counts it finished
+    auto count_fin = [&]() {
+        if (kQueue && (a.fin_flags & 1u)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(&s_fin, 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t + 1u == (uint32_t)kWaves && lane == 0)
+                __hip_atomic_fetch_add(&a.st->fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    if (wave != 0) {
+        count_fin();
+        return;
+    }
     // ---- wave 0: flush the workgroup into the replicated accumulators ----
+    // (a queue launch after the first does its between-batch bookkeeping here, once the
+    // previous launch has finished: before its own count, so before the next launch's atomics)
+    if (q_wait && blockIdx.x < 8) books();
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
     // so every accumulator kind goes out as ONE instruction, lane k carrying field k.  Nothing
     // waits for them: the next launch reads them (kernel boundary), the host after a
@@ -1813,15 +1898,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // the workgroup's last table hit per family (the next launch reads the one the batch
     // maximum points at)
     if ((lane < 3 && x4) || (lane >= 3 && lane < kPayWords && x6))
-        reinterpret_cast<uint32_t*>(&pay_cur(a)[blockIdx.x])[lane] = s_pay[lane < 3 ? w4 : w6][lane];
+        st_wt(&reinterpret_cast<uint32_t*>(&pay_cur(a)[blockIdx.x])[lane], s_pay[lane < 3 ? w4 : w6][lane]);
     // workgroup 0: the folded starting state for batch k + 1 (which folds this batch's outcome
     // into it)
+    if (blockIdx.x == 0 && lane < 16) {
+        // lane j: word j (written through, as the payloads)
+        uint32_t v = 0u;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) v = lane == j ? L1[j] : v;
+        st_wt(&reinterpret_cast<uint32_t*>(l1_out(a))[lane], v);
+    }
     if (blockIdx.x == 0 && lane == 0) {
-        uint4* o = reinterpret_cast<uint4*>(l1_out(a));
-        o[0] = make_uint4(L1[0], L1[1], L1[2], L1[3]);
-        o[1] = make_uint4(L1[4], L1[5], L1[6], L1[7]);
-        o[2] = make_uint4(L1[8], L1[9], L1[10], 0u);
-        o[3] = make_uint4(0u, 0u, 0u, 0u);
         // tell the host whether this batch started from agreeing entries (upe_gpu_process picks
         // the kernel without look-back once one has)
         if (!kNoLB && a.agree_out)
@@ -1829,6 +1916,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                a.launch_tag << 2 | (L1[9] ? 1ull : 0ull) | (L1[10] ? 2ull : 0ull),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    count_fin();
     STAMP(5);
 }
 
@@ -2208,6 +2296,18 @@ struct upe_gpu_ctx {
     uint32_t last_grid = 0;
     unsigned long long* ring_wg = nullptr;   // ring launches: per-batch counters + time origin
     size_t ring_alloc = 0;
+    // overlapped launches (upe_gpu_process_queue_emit): the finished / started workgroup counts
+    // st->fin / st->started will have reached once the launches queued so far have run, the
+    // flags and wait of the next launch, the queue's second stream, the signal word the next
+    // launch's stream waits on, and the stream of the queue's previous launch (while one runs)
+    uint32_t fin_total = 0, start_total = 0;
+    uint32_t fin_next_flags = 0, fin_next_wait = 0;
+    hipStream_t q_stream = nullptr;
+    hipEvent_t q_ev = nullptr;
+    unsigned long long* sig = nullptr;
+    hipStream_t q_prev = nullptr;
+    int overlap = -1;              // UPE_GPU_OVERLAP (default 1) and device support; -1 unknown
+    uint32_t overlapped = 0;       // launches that waited for their predecessor (launch_info)
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
@@ -2356,7 +2456,7 @@ int order_on(upe_gpu_ctx* c, hipStream_t s) {
 }
 
 // The state slots of batch k (DevState comment).
-DevL1* l1_slot(upe_gpu_ctx* c, uint64_t k) { return &c->st->l1[k % 2]; }
+DevL1* l1_slot(upe_gpu_ctx* c, uint64_t k) { return &c->st->l1[k % 2].s; }
 BatchAcc* acc_slot(upe_gpu_ctx* c, uint64_t k) { return &c->st->acc[k % 3]; }
 TilePay* pay_slot(upe_gpu_ctx* c, uint64_t k) { return c->pay + (size_t)(k % 2) * c->paycap; }
 
@@ -2401,16 +2501,18 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 32;
+constexpr int kVarCount = 64;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
-// bit 4 ring (lean emit linear scan only).
-int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false) {
-    return (ring ? 16 : 0) | (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+// bit 4 ring (lean emit linear scan only), bit 5 queue (overlapped launches; emit only).
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool queue = false) {
+    return (queue && emit ? 32 : 0) | (ring ? 16 : 0) | (lean && nolb ? 8 : 0) | (lean ? 4 : 0) |
+           (tss ? 2 : 0) | (emit ? 1 : 0);
 }
 template <int V>
 const void* classify_fn_of() {
     return reinterpret_cast<const void*>(
-        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0>);
+        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0,
+                      (V & 32) != 0>);
 }
 const void* classify_fn(int var) {
     static const void* const fns[kVarCount] = {
@@ -2419,7 +2521,13 @@ const void* classify_fn(int var) {
         nullptr, nullptr, nullptr, nullptr,
         classify_fn_of<12>(), classify_fn_of<13>(), classify_fn_of<14>(), classify_fn_of<15>(),
         nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<21>(), nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<29>(), nullptr, nullptr};
+        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<29>(), nullptr, nullptr,
+        // queue variants (emit)
+        nullptr, classify_fn_of<33>(), nullptr, classify_fn_of<35>(),
+        nullptr, classify_fn_of<37>(), nullptr, classify_fn_of<39>(),
+        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<45>(), nullptr, classify_fn_of<47>(),
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return var >= 0 && var < kVarCount ? fns[var] : nullptr;
 }
 
@@ -2442,10 +2550,15 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
 // launch the first time the configuration is used (census_probe).  0 on error.
 uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
-    static_assert(kVarCount <= 32, "the variant takes the key's low 5 bits");
-    const uint64_t key = (uint64_t)lds << 5 | (uint64_t)var;
+    static_assert(kVarCount <= 64, "the variant takes the key's low 6 bits");
+    const uint64_t key = (uint64_t)lds << 6 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
+    // a census counts what an idle chip holds: let an overlapped queue's previous launch finish
+    if (c->q_prev && hipStreamSynchronize(c->q_prev) != hipSuccess) {
+        fail("census: synchronising the previous launch failed");
+        return 0;
+    }
     int per_cu = 0;
     hipError_t e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, classify_fn(var), kBlock, lds);
@@ -2684,6 +2797,9 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     }
     if (c->s_in) (void)hipStreamSynchronize(c->s_in), (void)hipStreamDestroy(c->s_in);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out), (void)hipStreamDestroy(c->s_out);
+    if (c->q_stream) (void)hipStreamSynchronize(c->q_stream), (void)hipStreamDestroy(c->q_stream);
+    if (c->q_ev) (void)hipEventDestroy(c->q_ev);
+    if (c->sig) (void)hipFree(c->sig);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->agree_h) (void)hipHostFree(c->agree_h);
     delete c;
@@ -3169,7 +3285,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             HIP_TRY(hipEventCreate(&e));
             c->ev.push_back(e);
         }
-        HIP_TRY(hipEventRecord(c->ev[c->ev_used], s));
+        // (in an overlapped queue, after the previous launch: the sample spans timing_span
+        // launch-to-launch intervals)
+        HIP_TRY(hipEventRecord(c->ev[c->ev_used], c->q_prev ? c->q_prev : s));
         c->t_left = c->timing_span;
     }
     Args a;
@@ -3264,14 +3382,15 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.launch_tag = c->k + 1;
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     bool stamp = ring && ring->done && emit && lean && !c->tss;
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp);
+    const bool queue = c->fin_next_flags != 0;   // a launch of upe_gpu_process_queue_emit
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3308,6 +3427,16 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             a.ring_done = ring->done;
             a.ring_t0 = c->ring_wg + nb;
         }
+    }
+    a.fin_flags = c->fin_next_flags;
+    a.fin_wait = c->fin_next_wait;
+    c->fin_next_flags = 0;
+    if (a.fin_flags & 1u) c->fin_total += grid;
+    if (a.fin_flags & 2u) ++c->overlapped;
+    if (a.fin_flags & 4u) {
+        c->start_total += grid;
+        a.start_target = c->start_total;
+        a.sig = c->sig;
     }
     launch_classify(var, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
@@ -3599,15 +3728,82 @@ int upe_gpu_process_batches(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list, con
     return 0;
 }
 
+int upe_gpu_process_queue_emit(upe_gpu_ctx_t* c, const upe_gpu_batch_t* batches, size_t count,
+                               void* stream) {
+    if (!c) return fail("null context");
+    if (count && !batches) return fail("null batch list");
+    DEV_SCOPE(c->device);
+    if (c->overlap < 0) {
+        const char* e = getenv("UPE_GPU_OVERLAP");
+        int can = 0;
+        c->overlap = (!e || atoi(e) != 0) &&
+                     hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue,
+                                           c->device) == hipSuccess && can;
+    }
+    // Overlap needs no group-by launches after each classify (they would read the shared length
+    // array while the next launch writes it) and one launch per batch.
+    bool ov = c->overlap == 1 && count > 1 && c->nrules_pad <= (uint32_t)kLdsStatsMax;
+    for (size_t k = 0; ov && k < count; ++k) ov = batches[k].n <= kMaxLaunch;
+    if (!ov) {
+        for (size_t k = 0; k < count; ++k)
+            if (process_impl(c, batches[k].frames, batches[k].desc, batches[k].verdict, nullptr,
+                             batches[k].hdr, batches[k].n, stream) != 0)
+                return -1;
+        return 0;
+    }
+    hipStream_t s0 = pick(c, stream);
+    if (!c->q_stream) HIP_TRY(hipStreamCreateWithFlags(&c->q_stream, hipStreamNonBlocking));
+    if (!c->q_ev) HIP_TRY(hipEventCreateWithFlags(&c->q_ev, hipEventDisableTiming));
+    if (!c->sig) {
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), 8, hipMallocSignalMemory));
+        HIP_TRY(hipMemset(c->sig, 0, 8));
+    }
+    // both streams after everything queued so far on the context
+    if (order_on(c, s0) != 0) return -1;
+    HIP_TRY(hipEventRecord(c->q_ev, s0));
+    HIP_TRY(hipStreamWaitEvent(c->q_stream, c->q_ev, 0));
+    hipStream_t prev = nullptr;
+    int rc = 0;
+    for (size_t k = 0; k < count && rc == 0; ++k) {
+        hipStream_t sk = (k & 1) ? c->q_stream : s0;
+        static const bool no_gate = getenv("UPE_GPU_DIAG_NO_GATE") != nullptr;   // diagnostic
+        if (k && !no_gate) {
+            // not before every workgroup of the previous launch is resident (its last one to
+            // start stores the previous launch's tag, c->k, into the signal word)
+            const hipError_t e = hipStreamWaitValue32(sk, c->sig, (uint32_t)c->k,
+                                                      hipStreamWaitValueGte, 0xFFFFFFFFu);
+            if (e != hipSuccess) {
+                rc = fail(std::string("hipStreamWaitValue32: ") + hipGetErrorString(e));
+                break;
+            }
+        }
+        c->fin_next_flags = 1u | 4u | (k ? 2u : 0u);
+        c->fin_next_wait = c->fin_total;
+        c->q_prev = prev;
+        c->last_stream = sk;   // ordered by the wait above, not by order_on's event
+        rc = process_impl(c, batches[k].frames, batches[k].desc, batches[k].verdict, nullptr,
+                          batches[k].hdr, batches[k].n, sk);
+        prev = sk;
+    }
+    c->q_prev = nullptr;
+    c->fin_next_flags = 0;
+    // the caller's stream after the queue's last launch
+    if (prev && prev != s0) {
+        HIP_TRY(hipEventRecord(c->q_ev, prev));
+        HIP_TRY(hipStreamWaitEvent(s0, c->q_ev, 0));
+    }
+    c->last_stream = s0;
+    return rc;
+}
+
 int upe_gpu_process_batches_emit(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list,
                                  const uint64_t* d_desc, uint32_t* d_verdict, upe_hdr_rec_t* d_hdr,
                                  size_t n, size_t count, void* stream) {
     if (!c) return fail("null context");
     if (count && !d_frames_list) return fail("null frames list");
-    for (size_t k = 0; k < count; ++k)
-        if (upe_gpu_process_emit(c, d_frames_list[k], d_desc, d_verdict, d_hdr, n, stream) != 0)
-            return -1;
-    return 0;
+    std::vector<upe_gpu_batch_t> q(count);
+    for (size_t k = 0; k < count; ++k) q[k] = upe_gpu_batch_t{d_frames_list[k], d_desc, d_verdict, d_hdr, n};
+    return upe_gpu_process_queue_emit(c, q.data(), count, stream);
 }
 
 #if UPE_STAMPS
@@ -3847,6 +4043,7 @@ int upe_gpu_launch_info(upe_gpu_ctx_t* c, upe_launch_info_t* info) {
     HIP_TRY(hipDeviceSynchronize());
     memset(info, 0, sizeof *info);
     info->launches = c->k;
+    info->overlapped = c->overlapped;
     if (c->k == 0 || c->last_var < 0) return 0;
     info->variant = (uint32_t)c->last_var;
     info->grid = c->last_grid;

@@ -26,6 +26,12 @@ LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
 VAR_NOLB = 8   # launch_info variant bit: the kernel without look-back
 
 
+class QueueBatch(ctypes.Structure):
+    """upe_gpu_batch_t (include/upe_gpu.h)."""
+    _fields_ = [("frames", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("verdict", ctypes.c_void_p), ("hdr", ctypes.c_void_p), ("n", ctypes.c_size_t)]
+
+
 class UpeGpuError(RuntimeError):
     pass
 
@@ -71,6 +77,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_emit": (I, [P, P, P, P, P, SZ, P]),
         "upe_gpu_process_batches_emit": (I, [P, P, P, P, P, SZ, SZ, P]),
         "upe_gpu_process_ring_emit": (I, [P, P, P, P, P, SZ, SZ, P, P]),
+        "upe_gpu_process_queue_emit": (I, [P, P, SZ, P]),
         "upe_hdr_apply": (None, [P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
@@ -104,7 +111,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_gpu_process_host_emit",
             "upe_gpu_process_batches", "upe_gpu_process_rss", "upe_gpu_compact",
             "upe_gpu_process_segmented", "upe_gpu_process_emit", "upe_gpu_process_batches_emit",
-            "upe_gpu_process_ring_emit",
+            "upe_gpu_process_ring_emit", "upe_gpu_process_queue_emit",
             "upe_hdr_apply",
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
@@ -247,6 +254,15 @@ class GpuWorker:
                                                 _dev_ptr(hdr), n, len(frames_ptrs),
                                                 stream or None),
                "upe_gpu_process_batches_emit")
+
+    def process_queue_emit(self, batches, stream=None) -> None:
+        """upe_gpu_process_queue_emit over a list of (frames, desc, verdict, hdr, n) device
+        buffers (pointers or tensors): the worker loop with consecutive launches overlapped."""
+        arr = (QueueBatch * len(batches))(*[QueueBatch(_dev_ptr(f), _dev_ptr(d), _dev_ptr(v),
+                                                       _dev_ptr(h), int(n))
+                                            for f, d, v, h, n in batches])
+        _check(LIB.upe_gpu_process_queue_emit(self._ctx, arr, len(batches), stream or None),
+               "upe_gpu_process_queue_emit")
 
     def process_ring_emit(self, frames, desc, verdict, hdr, n: int, count: int, done_ns=None,
                           stream=None) -> None:

@@ -56,7 +56,7 @@ BATCH_INFO_DTYPE = np.dtype([("counters", COUNTERS_DTYPE), ("n_ctrl", "<u8"),
                              ("first_ctrl", "<u8")])
 # upe_launch_info_t (include/upe_gpu.h)
 LAUNCH_INFO_DTYPE = np.dtype([("variant", "<u4"), ("grid", "<u4"), ("deferred", "<u4"),
-                              ("reserved", "<u4"), ("launches", "<u8")])
+                              ("overlapped", "<u4"), ("launches", "<u8")])
 
 # verdict word (include/upe_gpu.h)
 V_DROP_PARSE, V_DROP_NOMATCH, V_DROP_RULE, V_DROP_TTL, V_FWD, V_CONSUMED, V_DROP_ACTION = range(7)
