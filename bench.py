@@ -252,6 +252,38 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool, apply_threa
             "times": times, "emit": emit, "apply_threads": apply_threads}
 
 
+def host_mapped(worker, wl, reps: int, emit: bool) -> dict:
+    """Host-inclusive rate without DMA copies: the batch lies in pinned host memory and the
+    classify kernel reads its descriptors and header windows, and writes the verdicts and the
+    rewritten header bytes (in place) or the records (emit), over the link itself
+    (upe_gpu_process_mapped[_emit]).  Full frames stay in host memory (no header-window
+    extraction); only the bytes the path touches cross the link."""
+    from upe_amd import gpu
+
+    pf = gpu.PinnedArray(wl.frames.shape, np.uint8)
+    pd = gpu.PinnedArray(wl.desc.shape, np.uint64)
+    pv = gpu.PinnedArray((wl.n,), np.uint32)
+    ph = gpu.PinnedArray((wl.n, 16), np.uint8) if emit else None
+    pd.array[:] = wl.desc
+    times = []
+    for r in range(reps + 2):
+        pf.array[:] = wl.frames           # untimed: a fresh batch every pass
+        t0 = time.perf_counter()
+        if emit:
+            worker.process_mapped_emit(pf.array, pd.array, pv.array, ph.array)
+        else:
+            worker.process_mapped(pf.array, pd.array, pv.array)
+        worker.sync()
+        t1 = time.perf_counter()
+        if r >= 2:
+            times.append(t1 - t0)
+    for x in (pf, pd, pv, ph):
+        if x is not None:
+            x.free()
+    return {"seconds": float(np.median(times)), "packets": wl.n, "times": times, "reps": reps,
+            "emit": emit}
+
+
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
              copies_cap: int) -> dict:
     """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
@@ -393,6 +425,9 @@ def main() -> None:
                          "emit-mode host round trip; -1: records returned, not applied")
     ap.add_argument("--no-host-emit", action="store_true",
                     help="skip the emit-mode host round trip")
+    ap.add_argument("--no-host-mapped", action="store_true",
+                    help="skip the mapped host legs (the kernel reading and writing pinned host "
+                         "memory itself, upe_gpu_process_mapped[_emit])")
     ap.add_argument("--workers-per-gpu", type=int, default=0,
                     help="also time W worker contexts sharing this GPU, each on its own stream "
                          "with its own batches and L1 state, as W reference worker threads would "
@@ -574,6 +609,19 @@ def main() -> None:
             hre = host_roundtrip(worker, wl, args.host_reps, args.host_chunk,
                                  windows=args.config != "B", apply_threads=args.host_apply_threads)
 
+    hm = hme = None
+    if args.host_reps > 0 and not args.no_host_mapped:
+        for emit_leg in (False, True):
+            worker.reset_stats()
+            if dist:
+                dist.barrier()
+            r = host_mapped(worker, wl, args.host_reps, emit_leg)
+            r["seconds"] = shard.max_over_ranks(r["seconds"], dist, dev)
+            if emit_leg:
+                hme = r
+            else:
+                hm = r
+
     # the job ends when the slowest shard does; value = every rank's packets / that time
     elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
     total_packets = float(shard.sum_over_ranks([n * args.steps], dist, dev)[0])
@@ -672,6 +720,21 @@ def main() -> None:
                       "the same output bytes as host_roundtrip" if hre["apply_threads"] >= 0 else
                       "not applied (frames untouched: a TX path sends each record as its own "
                       "iovec)"))
+        for key, h, what in (
+                ("host_mapped", hm, "frames rewritten in place in host memory"),
+                ("host_mapped_emit", hme, "verdicts + 16-B records written to host memory, frames "
+                                          "read only")):
+            if h:
+                out[key] = {"value": round(h["packets"] * world / h["seconds"] / 1e6, 2),
+                            "unit": "Mpps", "ms_per_batch": round(h["seconds"] * 1e3, 3),
+                            "ms_min_max": [round(min(h["times"]) * 1e3, 3),
+                                           round(max(h["times"]) * 1e3, 3)],
+                            "frame_bytes_in_host_memory": int(wl.frames.nbytes),
+                            "what": "pinned host batch (full frames) classified where it lies: the "
+                                    "kernel's own loads and stores over the link, no DMA copy "
+                                    "(upe_gpu_process_mapped" + ("_emit" if h["emit"] else "") +
+                                    "); " + what + f"; median of {h['reps']} passes, all ranks "
+                                    "at once"}
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             # config A is the reference's one-worker pcap replay: time it on one core
             out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads,

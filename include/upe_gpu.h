@@ -307,9 +307,33 @@ int upe_gpu_process_host_emit(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t fram
                               const uint64_t *h_desc, uint32_t *h_verdict, upe_hdr_rec_t *h_hdr,
                               size_t n, size_t chunk, int apply_threads);
 
-/* Pinned (page-locked) host memory for upe_gpu_process_host() batches. */
+/* Pinned (page-locked) host memory for upe_gpu_process_host() batches; the GPU can also read and
+ * write it directly (upe_gpu_process_mapped). */
 void *upe_gpu_host_alloc(size_t bytes);
 int upe_gpu_host_free(void *ptr);
+
+/* Page-lock an existing host buffer and map it for the GPU (e.g. the reference's pktbuf pool,
+ * src/pktbuf.c: pool->mem), so that upe_gpu_process_mapped() can classify its frames where they
+ * lie.  `ptr` and `bytes` need no alignment.  0 / -1. */
+int upe_gpu_host_register(void *ptr, size_t bytes);
+int upe_gpu_host_unregister(void *ptr);
+
+/* The batch in host memory, classified by the kernel's own loads over the link: no DMA copies and
+ * no staging slots.  The kernel reads each frame's header window and its descriptor from host
+ * memory and writes the verdicts (and in place: the rewritten header bytes, exactly as
+ * upe_gpu_process() does in HBM; emit: the 16-byte records) straight into host memory, so only
+ * the bytes the path touches cross the link — for long frames a fraction of the frame span the
+ * DMA round trip must copy.  Every pointer is host memory from upe_gpu_host_alloc() or
+ * upe_gpu_host_register() (checked: -1 otherwise); layout and UPE_FRAME_TAIL rule as for
+ * upe_gpu_process().  Asynchronous on `stream` like upe_gpu_process(): the outputs are the
+ * host's to read after upe_gpu_sync().  This replaces the worker's burst loop over pktbufs in the
+ * pool (src/worker.c:255-307) with nothing copied: the frames are rewritten where tx_send reads
+ * them (src/tx_afpacket.c:60-76). */
+int upe_gpu_process_mapped(upe_gpu_ctx_t *ctx, uint8_t *h_frames, const uint64_t *h_desc,
+                           uint32_t *h_verdict, size_t n, void *stream);
+int upe_gpu_process_mapped_emit(upe_gpu_ctx_t *ctx, uint8_t *h_frames, const uint64_t *h_desc,
+                                uint32_t *h_verdict, upe_hdr_rec_t *h_hdr, size_t n,
+                                void *stream);
 
 /* Queue `count` batches back to back from native code: batch k is d_frames_list[k] (a host
  * array of device pointers), all sharing one descriptor array and one verdict array (each batch
@@ -345,8 +369,11 @@ typedef struct upe_gpu_batch {
  * and the L1 state — equal `count` upe_gpu_process_emit() calls in order; batches may share
  * descriptor and output buffers (each batch's stores come after the previous batch's finished).
  * Falls back to sequential launches for tables of more than 4096 rules (their rule_stats
- * group-by follows each launch), batches over 2^24 packets, or UPE_GPU_OVERLAP=0.  `stream`
- * orders the queue after earlier work and everything after it.  0 / -1. */
+ * group-by follows each launch) or batches over 2^24 packets.  The overlap is opt-in
+ * (environment UPE_GPU_OVERLAP=1): on MI355X it measured slower than one launch after another
+ * (config B 25.2 vs 24.2 us per batch, C 45 vs 39), so by default the batches run
+ * as sequential upe_gpu_process_emit() launches.  `stream` orders the queue after earlier work
+ * and everything after it.  0 / -1. */
 int upe_gpu_process_queue_emit(upe_gpu_ctx_t *ctx, const upe_gpu_batch_t *batches, size_t count,
                                void *stream);
 

@@ -21,6 +21,12 @@ from upe_amd.layout import desc_offsets
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _overlap_on(monkeypatch):
+    """The overlap is opt-in (read when a context first queues): these tests exercise it."""
+    monkeypatch.setenv("UPE_GPU_OVERLAP", "1")
+
+
 def _run(w, wl, bounds, queue: bool):
     """The workload's batches [bounds[i], bounds[i+1]) as one queue or one call each; returns
     (frames, verdict, records) of the whole stream."""

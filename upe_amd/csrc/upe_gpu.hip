@@ -154,6 +154,14 @@ constexpr bool kVerdictSc1 = UPE_VERDICT_SC1;
 #ifndef UPE_DIAG_NO_DONE
 #define UPE_DIAG_NO_DONE 0   // diagnostic timing builds only: no deferred-candidate repair
 #endif
+// Overlapped queue launches: s_sleep argument (units of 64 clocks) between wave 0's polls of the
+// previous launch's finished-workgroup count.
+#ifndef UPE_DIAG_Q_NOWAIT
+#define UPE_DIAG_Q_NOWAIT 0   // diagnostic timing builds only: queue launches do not wait
+#endif
+#ifndef UPE_Q_POLL_SLEEP
+#define UPE_Q_POLL_SLEEP 4
+#endif
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
 // rv4[i]: header + first address word, used for every packet:
@@ -1201,6 +1209,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
     __shared__ uint32_t s_bdone[kRing ? 4 : 1];   // ring: chunks finished per batch (4 in flight)
     __shared__ uint32_t s_fin;     // queue launches: waves finished (fin_flags bit 0)
+    __shared__ uint32_t s_qready;  // queue launches: wave 0 has seen the previous launch finish
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -1285,6 +1294,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     };
     if (tid == 0) s_claim = kWaves;
     if (kQueue && tid == 0) s_fin = 0u;
+    if (kQueue && tid == 0) s_qready = 0u;
     if (kRing && tid < 4) s_bdone[tid] = 0u;
     if (kRing && tid == 0)   // the ring's time origin: the first workgroup to start
         __hip_atomic_fetch_min(a.ring_t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
@@ -1383,10 +1393,24 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             // of the previous one's (L1 state, accumulators, payloads) was stored write-through
             // or by atomics and drained before that count, on lines nothing here has touched
             // since this launch began.
-            while ((int32_t)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                 &a.st->fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
-                             a.fin_wait) < 0)
-                __builtin_amdgcn_s_sleep(2);
+            // One poller per workgroup (wave 0, which always reaches this point: with its first
+            // chunk or after the loop); the other waves wait for its word in LDS.  (Every wave
+            // polling the one device word put ~70 k loads per us on one memory channel while the
+            // previous launch's tail was still running through it.)
+            if (UPE_DIAG_Q_NOWAIT) {
+                // diagnostic timing builds only: no wait (results wrong)
+            } else if (wave == 0) {
+                while ((int32_t)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                     &a.st->fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
+                                 a.fin_wait) < 0)
+                    __builtin_amdgcn_s_sleep(UPE_Q_POLL_SLEEP);
+                if (lane == 0)
+                    __hip_atomic_store(&s_qready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                           &s_qready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
+                    __builtin_amdgcn_s_sleep(2);
+            }
             load_prev();
         }
         if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
@@ -2306,7 +2330,7 @@ struct upe_gpu_ctx {
     hipEvent_t q_ev = nullptr;
     unsigned long long* sig = nullptr;
     hipStream_t q_prev = nullptr;
-    int overlap = -1;              // UPE_GPU_OVERLAP (default 1) and device support; -1 unknown
+    int overlap = -1;              // UPE_GPU_OVERLAP (default 0) and device support; -1 unknown
     uint32_t overlapped = 0;       // launches that waited for their predecessor (launch_info)
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
@@ -2342,6 +2366,7 @@ struct upe_gpu_ctx {
     // host threads applying emit-mode records to the caller's frames (upe_gpu_process_host_emit)
     std::unique_ptr<struct ApplyPool> pool;
     uint32_t host_slots = 4;       // device slots of the host round trip (UPE_GPU_HOST_SLOTS, 2..8)
+    int host_serial = -1;          // UPE_GPU_HOST_SERIAL: copies back on the copy-in stream (-1: per mode)
     // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
     // device into host-mapped memory, and the first launch whose report counts
     unsigned long long* agree_h = nullptr;
@@ -2725,6 +2750,7 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
         if (const char* v = getenv("UPE_GPU_LB_SPIN")) c->lb_spin = (uint32_t)strtoul(v, nullptr, 10);
         if (const char* v = getenv("UPE_GPU_LB_SYNC")) c->lb_sync = v[0] == '1';
         if (const char* v = getenv("UPE_GPU_NOLB")) c->allow_nolb = v[0] != '0';
+        if (const char* v = getenv("UPE_GPU_HOST_SERIAL")) c->host_serial = atoi(v) != 0;
         if (const char* v = getenv("UPE_GPU_HOST_SLOTS"))
             c->host_slots = std::min(8u, std::max(2u, (uint32_t)strtoul(v, nullptr, 10)));
     }
@@ -3565,6 +3591,10 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         }
     } drain{c};
     const size_t nslots = c->host_slots;
+    // the stream the copies back go to: the copy-out stream (both link directions at once), or
+    // the copy-in stream, one direction at a time
+    const bool serial = c->host_serial < 0 ? false : c->host_serial != 0;
+    hipStream_t s_back = serial ? c->s_in : c->s_out;
     const size_t lag = 2;   // emit: chunk k - lag is applied while chunk k is issued
     struct Done {
         size_t s, e, slot;
@@ -3596,6 +3626,32 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
                                       len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT,
                                       hipMemcpyDeviceToHost));
                 }
+        return 0;
+    };
+    // a chunk's copy-back (verdicts + records, or verdicts + the rewritten span), once its kernel
+    // is queued
+    struct Back {
+        bool pending;
+        size_t s, e, slot;
+        uint64_t lo, wb;
+    } back{false, 0, 0, 0, 0, 0};
+    auto issue_back = [&]() -> int {
+        auto& sb = c->hs[back.slot];
+        const size_t m = back.e - back.s;
+        back.pending = false;
+        HIP_TRY(hipStreamWaitEvent(s_back, sb.k_done, 0));
+        HIP_TRY(hipMemcpyAsync(h_verdict + back.s, sb.verdict, m * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s_back));
+        if (emit)
+            HIP_TRY(hipMemcpyAsync(h_hdr + back.s, sb.hdr, m * sizeof(upe_hdr_rec_t),
+                                   hipMemcpyDeviceToHost, s_back));
+        else
+            HIP_TRY(hipMemcpyAsync(h_frames + back.lo, sb.frames, (size_t)(back.wb - back.lo),
+                                   hipMemcpyDeviceToHost, s_back));
+        HIP_TRY(hipEventRecord(sb.out_done, s_back));
+        sb.busy = true;
+        sb.lo = back.lo;
+        sb.wb = back.wb;
         return 0;
     };
     size_t k = 0;
@@ -3651,6 +3707,9 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         // landed: its own copy-back rewrites its whole span, and would otherwise put back the
         // earlier chunk's frames as they were before they were processed.  (Emit mode copies
         // no frame bytes back.)
+        // (a copy-back still deferred, serial mode, goes first if this chunk's bytes interleave
+        // with its chunk's: on the same stream, it then lands before this chunk is read)
+        if (back.pending && !emit && back.lo < hi && lo < back.wb && issue_back() != 0) return -1;
         if (!emit)
             for (auto& other : c->hs)
                 if (&other != &sl && other.busy && other.lo < hi && lo < other.wb)
@@ -3667,24 +3726,17 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
                  : upe_gpu_process(c, base, sl.desc, sl.verdict, m, nullptr))
             return -1;
         HIP_TRY(hipEventRecord(sl.k_done, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->s_out, sl.k_done, 0));
-        HIP_TRY(hipMemcpyAsync(h_verdict + s, sl.verdict, m * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, c->s_out));
-        if (emit)
-            HIP_TRY(hipMemcpyAsync(h_hdr + s, sl.hdr, m * sizeof(upe_hdr_rec_t),
-                                   hipMemcpyDeviceToHost, c->s_out));
-        else
-            HIP_TRY(hipMemcpyAsync(h_frames + lo, sl.frames, (size_t)(wb - lo),
-                                   hipMemcpyDeviceToHost, c->s_out));
-        HIP_TRY(hipEventRecord(sl.out_done, c->s_out));
-        sl.busy = true;
-        sl.lo = lo;
-        sl.wb = wb;
+        // serial mode: this chunk's copy-back is issued after the next chunk's copy-in, so that
+        // the copy-in stream never idles while a kernel runs
+        if (back.pending && issue_back() != 0) return -1;
+        back = Back{true, s, e, si, lo, wb};
+        if (!serial && issue_back() != 0) return -1;
         if (emit) pending.push_back(Done{s, e, si, lo});
     }
+    if (back.pending && issue_back() != 0) return -1;
     for (const Done& d : pending)
         if (finish(d) != 0) return -1;
-    HIP_TRY(hipStreamSynchronize(c->s_out));
+    HIP_TRY(hipStreamSynchronize(s_back));
     return 0;
 }
 }  // namespace
@@ -3719,6 +3771,67 @@ int upe_gpu_host_free(void* p) {
     return 0;
 }
 
+int upe_gpu_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return fail("null or empty host buffer");
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    return 0;
+}
+
+int upe_gpu_host_unregister(void* p) {
+    if (!p) return fail("null host buffer");
+    HIP_TRY(hipHostUnregister(p));
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+// The device address of page-locked, mapped host memory; nullptr (and an error) for anything
+// else, so that a kernel never dereferences an unmapped host address.
+template <typename T>
+T* mapped(T* h, const char* what) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(static_cast<const void*>(h)), 0) != hipSuccess ||
+        !d) {
+        (void)hipGetLastError();
+        fail(std::string(what) + " is not pinned, mapped host memory (upe_gpu_host_alloc / "
+             "upe_gpu_host_register)");
+        return nullptr;
+    }
+    return static_cast<T*>(d);
+}
+}  // namespace
+
+extern "C" {
+
+int upe_gpu_process_mapped(upe_gpu_ctx_t* c, uint8_t* h_frames, const uint64_t* h_desc,
+                           uint32_t* h_verdict, size_t n, void* stream) {
+    if (!c) return fail("null context");
+    DEV_SCOPE(c->device);
+    if (n == 0) return upe_gpu_process(c, nullptr, nullptr, nullptr, 0, stream);
+    if (!h_frames || !h_desc || !h_verdict) return fail("null host buffer");
+    uint8_t* f = mapped(h_frames, "h_frames");
+    const uint64_t* d = f ? mapped(h_desc, "h_desc") : nullptr;
+    uint32_t* v = d ? mapped(h_verdict, "h_verdict") : nullptr;
+    if (!v) return -1;
+    return process_impl(c, f, d, v, nullptr, nullptr, n, stream);
+}
+
+int upe_gpu_process_mapped_emit(upe_gpu_ctx_t* c, uint8_t* h_frames, const uint64_t* h_desc,
+                                uint32_t* h_verdict, upe_hdr_rec_t* h_hdr, size_t n,
+                                void* stream) {
+    if (!c) return fail("null context");
+    DEV_SCOPE(c->device);
+    if (n == 0) return upe_gpu_process(c, nullptr, nullptr, nullptr, 0, stream);
+    if (!h_frames || !h_desc || !h_verdict || !h_hdr) return fail("null host buffer");
+    uint8_t* f = mapped(h_frames, "h_frames");
+    const uint64_t* d = f ? mapped(h_desc, "h_desc") : nullptr;
+    uint32_t* v = d ? mapped(h_verdict, "h_verdict") : nullptr;
+    upe_hdr_rec_t* h = v ? mapped(h_hdr, "h_hdr") : nullptr;
+    if (!h) return -1;
+    return process_impl(c, f, d, v, nullptr, h, n, stream);
+}
+
 int upe_gpu_process_batches(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list, const uint64_t* d_desc,
                             uint32_t* d_verdict, size_t n, size_t count, void* stream) {
     if (!c) return fail("null context");
@@ -3736,7 +3849,8 @@ int upe_gpu_process_queue_emit(upe_gpu_ctx_t* c, const upe_gpu_batch_t* batches,
     if (c->overlap < 0) {
         const char* e = getenv("UPE_GPU_OVERLAP");
         int can = 0;
-        c->overlap = (!e || atoi(e) != 0) &&
+        // opt-in: measured slower than sequential launches on MI355X
+        c->overlap = (e && atoi(e) != 0) &&
                      hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue,
                                            c->device) == hipSuccess && can;
     }
@@ -3766,8 +3880,7 @@ int upe_gpu_process_queue_emit(upe_gpu_ctx_t* c, const upe_gpu_batch_t* batches,
     int rc = 0;
     for (size_t k = 0; k < count && rc == 0; ++k) {
         hipStream_t sk = (k & 1) ? c->q_stream : s0;
-        static const bool no_gate = getenv("UPE_GPU_DIAG_NO_GATE") != nullptr;   // diagnostic
-        if (k && !no_gate) {
+        if (k && !(UPE_DIAG_Q_NOWAIT && getenv("UPE_GPU_DIAG_NO_GATE"))) {
             // not before every workgroup of the previous launch is resident (its last one to
             // start stores the previous launch's tag, c->k, into the signal word)
             const hipError_t e = hipStreamWaitValue32(sk, c->sig, (uint32_t)c->k,

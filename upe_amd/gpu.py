@@ -81,6 +81,10 @@ def _load() -> ctypes.CDLL:
         "upe_hdr_apply": (None, [P, P]),
         "upe_gpu_host_alloc": (P, [SZ]),
         "upe_gpu_host_free": (I, [P]),
+        "upe_gpu_host_register": (I, [P, SZ]),
+        "upe_gpu_host_unregister": (I, [P]),
+        "upe_gpu_process_mapped": (I, [P, P, P, P, SZ, P]),
+        "upe_gpu_process_mapped_emit": (I, [P, P, P, P, P, SZ, P]),
     }
     sig.update({
         "upe_rules_load_ini": (I, [ctypes.c_char_p, P, SZ, P]),
@@ -115,7 +119,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_hdr_apply",
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
-            "upe_gpu_host_alloc", "upe_gpu_host_free")
+            "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
+            "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit")
 
 
 def _check(rc: int, what: str) -> None:
@@ -232,6 +237,24 @@ class GpuWorker:
         _check(LIB.upe_gpu_process(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
                                    _dev_ptr(verdict), n, stream or None),
                "upe_gpu_process")
+
+    def process_mapped(self, frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray,
+                       stream=None) -> None:
+        """upe_gpu_process_mapped: the batch classified where it lies in pinned host memory
+        (PinnedArray views or registered buffers), frames rewritten in place; asynchronous, read
+        the outputs after sync()."""
+        _check(LIB.upe_gpu_process_mapped(self._ctx, _np_ptr(frames), _np_ptr(desc),
+                                          _np_ptr(verdict), int(desc.shape[0]), stream or None),
+               "upe_gpu_process_mapped")
+
+    def process_mapped_emit(self, frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray,
+                            hdr: np.ndarray, stream=None) -> None:
+        """upe_gpu_process_mapped_emit: the same with 16-byte records into `hdr` (host), frames
+        read only."""
+        _check(LIB.upe_gpu_process_mapped_emit(self._ctx, _np_ptr(frames), _np_ptr(desc),
+                                               _np_ptr(verdict), _np_ptr(hdr),
+                                               int(desc.shape[0]), stream or None),
+               "upe_gpu_process_mapped_emit")
 
     def process_emit(self, frames, desc, verdict, hdr, n: int, stream=None) -> None:
         """Emit mode: rewritten header bytes into `hdr` (n 16-byte records), frames read only."""
@@ -437,6 +460,23 @@ class PinnedArray:
         if self.ptr:
             self.array = None
             LIB.upe_gpu_host_free(self.ptr)
+            self.ptr = None
+
+
+class RegisteredArray:
+    """An existing numpy array page-locked and mapped for the GPU (upe_gpu_host_register) until
+    free()."""
+
+    def __init__(self, array: np.ndarray):
+        assert array.flags["C_CONTIGUOUS"]
+        self.array = array
+        self.ptr = array.ctypes.data
+        _check(LIB.upe_gpu_host_register(self.ptr, max(int(array.nbytes), 1)),
+               "upe_gpu_host_register")
+
+    def free(self) -> None:
+        if self.ptr:
+            _check(LIB.upe_gpu_host_unregister(self.ptr), "upe_gpu_host_unregister")
             self.ptr = None
 
 
