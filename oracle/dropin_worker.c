@@ -8,7 +8,9 @@
  * What it shows: a reference worker_t, fed through the reference SPSC ring by an RX-like
  * producer thread exactly as src/rx_pcap.c feeds it (pktbuf_alloc, memcpy, ring_push_burst),
  * runs a GPU-backed worker loop instead of src/worker.c:255-307 — ring_pop_burst bursts
- * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch (cut
+ * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch (or, in
+ * mapped mode, upe_dropin_set_mapped(1): the pool registered once with upe_gpu_host_register and
+ * each batch's pktbufs classified where they lie by upe_gpu_process_mapped, nothing copied) (cut
  * after every packet that writes a neighbour table, whose write is then applied with the
  * reference's own arp_update / ndp_update and the snapshot re-uploaded), then the reference's TX
  * accounting (tx_send_batch, pkts_forwarded / pkts_dropped, pktbuf_free, tx_send of ARP
@@ -21,6 +23,7 @@
 #include <arpa/inet.h>
 #include <pthread.h>
 #include <signal.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -53,7 +56,13 @@ typedef struct {
     worker_t *w;
     int device;
     int rc;
+    uint8_t *pool_base; /* mapped mode: the registered pktbuf array (frames classified in place) */
 } gpu_arg_t;
+
+/* 0: header windows through upe_gpu_process_host (copies); 1: the pktbufs classified where they
+ * lie in the registered pool (upe_gpu_process_mapped, nothing copied). */
+static int g_mapped = 0;
+void upe_dropin_set_mapped(int mapped) { g_mapped = mapped; }
 
 /* The TX flush of the reference worker loop, src/worker.c:286-303. */
 static void flush_tx(worker_t *w) {
@@ -125,6 +134,7 @@ typedef struct {
     uint32_t *verdict;
     pktbuf_t **bufs;
     size_t n;
+    uint8_t *pool_base; /* mapped mode */
 } gpu_batch_t;
 
 /* One GPU batch through the host round trip, then the reference's per-verdict handling
@@ -132,13 +142,23 @@ typedef struct {
  * a table-writing control packet, that packet's writes and the new table snapshot. */
 static int run_batch(worker_t *w, gpu_batch_t *g, int cut) {
     if (g->n == 0) return 0;
-    if (upe_gpu_process_host(g->ctx, g->win, g->n * WIN + UPE_FRAME_TAIL, g->desc, g->verdict,
-                             g->n, 0) != 0)
+    if (g->pool_base) {
+        /* the frames rewritten in place in the pool, where tx_send reads them */
+        if (upe_gpu_process_mapped(g->ctx, g->pool_base, g->desc, g->verdict, g->n, NULL) != 0 ||
+            upe_gpu_sync(g->ctx, NULL) != 0) {
+            fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
+            return -1;
+        }
+    } else if (upe_gpu_process_host(g->ctx, g->win, g->n * WIN + UPE_FRAME_TAIL, g->desc,
+                                    g->verdict, g->n, 0) != 0) {
+        fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
         return -1;
+    }
     for (size_t i = 0; i < g->n; i++) {
         pktbuf_t *b = g->bufs[i];
         const uint32_t v = g->verdict[i];
-        memcpy(b->data, g->win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
+        if (!g->pool_base)
+            memcpy(b->data, g->win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
         if (cut && i + 1 == g->n) control_writes(w, b, v);
         if (UPE_VERDICT_CODE(v) == UPE_V_FWD) {
             w->tx_frames[w->tx_count] = b->data; /* worker.c:240-243 */
@@ -169,6 +189,7 @@ static void *gpu_worker_main(void *arg) {
     g.desc = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint64_t));
     g.verdict = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint32_t));
     g.bufs = malloc(GPU_BATCH * sizeof(*g.bufs));
+    g.pool_base = ga->pool_base;
     if (!g.ctx || !g.win || !g.desc || !g.verdict || !g.bufs) return NULL;
     if (upe_gpu_load_rules(g.ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
         load_tables(g.ctx, w) != 0 || upe_gpu_set_port(g.ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0)
@@ -179,10 +200,15 @@ static void *gpu_worker_main(void *arg) {
         w->pkts_in += k;                                                   /* worker.c:280 */
         for (unsigned j = 0; j < k; j++) {
             pktbuf_t *b = burst[j];
-            size_t c = b->len < WIN ? b->len : WIN;
-            memcpy(g.win + g.n * WIN, b->data, c);
-            memset(g.win + g.n * WIN + c, 0, WIN - c);
-            g.desc[g.n] = UPE_DESC((uint64_t)g.n * WIN, b->len);
+            if (g.pool_base) {
+                /* the pktbuf's data where it lies: offset into the registered pool */
+                g.desc[g.n] = UPE_DESC((uint64_t)(b->data - g.pool_base), b->len);
+            } else {
+                size_t c = b->len < WIN ? b->len : WIN;
+                memcpy(g.win + g.n * WIN, b->data, c);
+                memset(g.win + g.n * WIN + c, 0, WIN - c);
+                g.desc[g.n] = UPE_DESC((uint64_t)g.n * WIN, b->len);
+            }
             g.bufs[g.n++] = b;
             const int cut = is_table_write(b);
             if ((cut || g.n == GPU_BATCH) && run_batch(w, &g, cut) != 0) return NULL;
@@ -240,10 +266,18 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
      * worker frees any, so the test does not lean on concurrent alloc/free in the pool. */
     static pktbuf_pool_t pool;
     static size_t pool_cap;
+    /* (slack: every finished worker thread takes up to LOCAL_CACHE_SIZE buffers with it in its
+     * thread-local cache, reference src/pktbuf.c:10) */
     if (pool_cap < n + 256) {
         if (pool_cap) return -1; /* one size per process */
-        if (pktbuf_pool_init(&pool, n + 256) != 0) return -1;
-        pool_cap = n + 256;
+        if (pktbuf_pool_init(&pool, n + 8192) != 0) return -1;
+        pool_cap = n + 8192;
+    }
+    /* mapped mode: the pool's buffers page-locked and mapped for the GPU once */
+    static int pool_registered;
+    if (g_mapped && !pool_registered) {
+        if (upe_gpu_host_register(pool.buffers, pool.capacity * sizeof(pktbuf_t)) != 0) return -1;
+        pool_registered = 1;
     }
     pktbuf_t **all = malloc((n ? n : 1) * sizeof(*all));
     if (!all) return -1;
@@ -263,7 +297,7 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     if (!w || worker_init(w, 0, -1, &ring, &pool, &rt, &tx, &arpt, &ndpt) != 0) return -1;
 
     g_stop = 0;
-    gpu_arg_t ga = {w, device, -1};
+    gpu_arg_t ga = {w, device, -1, g_mapped ? (uint8_t *)pool.buffers : NULL};
     pthread_t th;
     pthread_create(&th, NULL, gpu_worker_main, &ga);
     /* producer: the RX thread's staged bursts of 32 into the ring, src/rx_pcap.c:80-92 */

@@ -29,6 +29,8 @@ def _lib():
     lib.upe_dropin_run.restype = ctypes.c_int
     lib.upe_dropin_run.argtypes = [P, SZ, SZ, P, SZ, P, SZ, P, ctypes.c_uint32, P, P, SZ,
                                    ctypes.c_int, P, P, P, P, P]
+    lib.upe_dropin_set_mapped.argtypes = [ctypes.c_int]
+    lib.upe_dropin_set_mapped.restype = None
     return lib
 
 
@@ -47,9 +49,14 @@ def _with_control(n, seed):
                                   lambda: _with_control(60_000, 63),
                                   lambda: synth.config_ndp_walk(repeat=20)],
                          ids=["B", "C", "C+control", "NS/NA opt_len wrap"])
-def test_reference_pipeline_with_gpu_worker(make):
+@pytest.mark.parametrize("mapped", [False, True], ids=["windows", "mapped-pool"])
+def test_reference_pipeline_with_gpu_worker(make, mapped):
+    """mapped-pool: the reference's pktbuf pool registered with upe_gpu_host_register and each
+    batch classified where its pktbufs lie (upe_gpu_process_mapped), frames rewritten in the pool
+    itself."""
     wl = make()
     lib = _lib()
+    lib.upe_dropin_set_mapped(1 if mapped else 0)
     rules = np.ascontiguousarray(wl.rules)
     eth = np.frombuffer(bytes(wl.eth_addr), np.uint8).copy()
     counters = np.zeros(5, np.uint64)
