@@ -422,7 +422,8 @@ int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
  * a bounded look-back; a wave that stops waiting (a workgroup it needs is not resident yet)
  * defers them, and the launch's last workgroup answers them. */
 typedef struct {
-    uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back */
+    uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back,
+                          4 ring, 5 queue, 6 a host path (upe_gpu_process_mapped / _host) */
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */

@@ -44,6 +44,8 @@ def _mapped_run(w, wl, emit: bool, registered: bool = False):
         else:
             w.process_mapped(f, d, v)
         w.sync()
+        if wl.n:
+            assert w.launch_info()["variant"] & gpu.VAR_HOST, "not the host-path kernel"
         frames = f.copy()
         verdict = v.copy()
         if emit:

@@ -478,16 +478,27 @@ __device__ __forceinline__ void store16(uint4* p, uint4 v) { *p = v; }
 #ifndef UPE_LOAD_NT
 #define UPE_LOAD_NT 0
 #endif
+// The host paths' launches (upe_gpu_process_mapped over host memory, ~1.3-1.5 ms per 1M packets,
+// link-bound; upe_gpu_process_host's chunks in device slots) run their own kernel instantiations
+// (variant bit 6), so that a profile keeps them apart from the device-resident launches of the
+// same configuration.  UPE_HOST_NT=1 makes their frame and descriptor loads
+// streaming (non-temporal) loads: measured slower (config B mapped 537 vs 666-680 Mpps in place,
+// C 214 vs 319; profiles/r03/v5_host_nt_ab.txt), so off.
+#ifndef UPE_HOST_NT
+#define UPE_HOST_NT 0
+#endif
+template <bool kHostMem = false>
 __device__ __forceinline__ uint4 ldf(const uint4* p) {
-    if (UPE_LOAD_NT & 1) {
+    if ((UPE_LOAD_NT & 1) || (kHostMem && UPE_HOST_NT)) {
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
         const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
         return make_uint4(x[0], x[1], x[2], x[3]);
     }
     return *p;
 }
+template <bool kHostMem = false>
 __device__ __forceinline__ uint64_t ldd(const uint64_t* p) {
-    if (UPE_LOAD_NT & 2) return __builtin_nontemporal_load(p);
+    if ((UPE_LOAD_NT & 2) || (kHostMem && UPE_HOST_NT)) return __builtin_nontemporal_load(p);
     return *p;
 }
 // The in-place header stores (diagnostic UPE_FRAME_SC1: written through, lines dropped from L2).
@@ -1197,7 +1208,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kQueue = false>
+          bool kQueue = false, bool kHost = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1239,7 +1250,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
                 if (c < 3 || len > 16u * c) {
-                    const uint4 v = ldf(&q[c]);
+                    const uint4 v = ldf<kHost>(&q[c]);
                     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
                 }
             }
@@ -1258,10 +1269,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            v.c0 = ldf(&q[0]); v.c1 = ldf(&q[1]); v.c2 = ldf(&q[2]);
+            v.c0 = ldf<kHost>(&q[0]); v.c1 = ldf<kHost>(&q[1]); v.c2 = ldf<kHost>(&q[2]);
             if (!kWin48) {
-                if (len > 48u) v.c3 = ldf(&q[3]);
-                if (len > 64u) v.c4 = ldf(&q[4]);
+                if (len > 48u) v.c3 = ldf<kHost>(&q[3]);
+                if (len > 64u) v.c4 = ldf<kHost>(&q[4]);
             }
         }
         return v;
@@ -1306,7 +1317,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // rule tables into LDS, before the entry barrier.  (Issuing the first chunk's window loads
     // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
     uint64_t dsc_next = 0;
-    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[ch * 64u + lane]);
+    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[ch * 64u + lane]);
     if (!kTssMode && small_stats) {
         const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
         const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
@@ -1492,7 +1503,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
         have_nw = false;
         dsc_next = 0;
-        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[chn * 64u + lane]);
+        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[chn * 64u + lane]);
         if (!folded) fold_start();
 
         if (first) STAMP_VM(2);
@@ -1821,7 +1832,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (late) {
             chn = claim();
             dsc_next = 0;
-            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd(&a.desc[chn * 64u + lane]);
+            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[chn * 64u + lane]);
             asm volatile("" : "+v"(dsc_next));   // consumed here (see before the loop)
         }
     }
@@ -2526,18 +2537,20 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 64;
+constexpr int kVarCount = 128;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
-// bit 4 ring (lean emit linear scan only), bit 5 queue (overlapped launches; emit only).
-int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool queue = false) {
-    return (queue && emit ? 32 : 0) | (ring ? 16 : 0) | (lean && nolb ? 8 : 0) | (lean ? 4 : 0) |
-           (tss ? 2 : 0) | (emit ? 1 : 0);
+// bit 4 ring (lean emit linear scan only), bit 5 queue (overlapped launches; emit only), bit 6
+// a host path's launch (upe_gpu_process_mapped / upe_gpu_process_host; not ring or queue).
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool queue = false,
+                 bool host = false) {
+    return (host && !ring && !queue ? 64 : 0) | (queue && emit ? 32 : 0) | (ring ? 16 : 0) |
+           (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
 }
 template <int V>
 const void* classify_fn_of() {
     return reinterpret_cast<const void*>(
         &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0,
-                      (V & 32) != 0>);
+                      (V & 32) != 0, (V & 64) != 0>);
 }
 const void* classify_fn(int var) {
     static const void* const fns[kVarCount] = {
@@ -2551,6 +2564,17 @@ const void* classify_fn(int var) {
         nullptr, classify_fn_of<33>(), nullptr, classify_fn_of<35>(),
         nullptr, classify_fn_of<37>(), nullptr, classify_fn_of<39>(),
         nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<45>(), nullptr, classify_fn_of<47>(),
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        // host-memory variants (upe_gpu_process_mapped[_emit])
+        classify_fn_of<64>(), classify_fn_of<65>(), classify_fn_of<66>(), classify_fn_of<67>(),
+        classify_fn_of<68>(), classify_fn_of<69>(), classify_fn_of<70>(), classify_fn_of<71>(),
+        nullptr, nullptr, nullptr, nullptr,
+        classify_fn_of<76>(), classify_fn_of<77>(), classify_fn_of<78>(), classify_fn_of<79>(),
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return var >= 0 && var < kVarCount ? fns[var] : nullptr;
@@ -2575,8 +2599,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
 // launch the first time the configuration is used (census_probe).  0 on error.
 uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
-    static_assert(kVarCount <= 64, "the variant takes the key's low 6 bits");
-    const uint64_t key = (uint64_t)lds << 6 | (uint64_t)var;
+    static_assert(kVarCount <= 128, "the variant takes the key's low 7 bits");
+    const uint64_t key = (uint64_t)lds << 7 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
     // a census counts what an idle chip holds: let an overlapped queue's previous launch finish
@@ -3274,7 +3298,7 @@ struct RingReq {
 };
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
-                 const RingReq* ring = nullptr) {
+                 const RingReq* ring = nullptr, bool host = false) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
@@ -3288,7 +3312,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             const size_t m = n - s0 < kMaxLaunch ? n - s0 : kMaxLaunch;
             if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
                              d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
-                             m, stream) != 0)
+                             m, stream, nullptr, host) != 0)
                 return -1;
         }
         return 0;
@@ -3409,14 +3433,14 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     bool stamp = ring && ring->done && emit && lean && !c->tss;
     const bool queue = c->fin_next_flags != 0;   // a launch of upe_gpu_process_queue_emit
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue);
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue, host);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue, host), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3722,8 +3746,9 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         // the descriptors keep their offsets relative to h_frames: hand the kernel a base that
         // maps offset lo onto the slot (lo is a multiple of 16, so the base stays aligned)
         uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.frames) - lo);
-        if (emit ? upe_gpu_process_emit(c, base, sl.desc, sl.verdict, sl.hdr, m, nullptr)
-                 : upe_gpu_process(c, base, sl.desc, sl.verdict, m, nullptr))
+        // (the host-path kernel instantiation: profiles keep these launches apart)
+        if (process_impl(c, base, sl.desc, sl.verdict, nullptr, emit ? sl.hdr : nullptr, m,
+                         nullptr, nullptr, true) != 0)
             return -1;
         HIP_TRY(hipEventRecord(sl.k_done, c->stream));
         // serial mode: this chunk's copy-back is issued after the next chunk's copy-in, so that
@@ -3814,7 +3839,7 @@ int upe_gpu_process_mapped(upe_gpu_ctx_t* c, uint8_t* h_frames, const uint64_t* 
     const uint64_t* d = f ? mapped(h_desc, "h_desc") : nullptr;
     uint32_t* v = d ? mapped(h_verdict, "h_verdict") : nullptr;
     if (!v) return -1;
-    return process_impl(c, f, d, v, nullptr, nullptr, n, stream);
+    return process_impl(c, f, d, v, nullptr, nullptr, n, stream, nullptr, true);
 }
 
 int upe_gpu_process_mapped_emit(upe_gpu_ctx_t* c, uint8_t* h_frames, const uint64_t* h_desc,
@@ -3829,7 +3854,7 @@ int upe_gpu_process_mapped_emit(upe_gpu_ctx_t* c, uint8_t* h_frames, const uint6
     uint32_t* v = d ? mapped(h_verdict, "h_verdict") : nullptr;
     upe_hdr_rec_t* h = v ? mapped(h_hdr, "h_hdr") : nullptr;
     if (!h) return -1;
-    return process_impl(c, f, d, v, nullptr, h, n, stream);
+    return process_impl(c, f, d, v, nullptr, h, n, stream, nullptr, true);
 }
 
 int upe_gpu_process_batches(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list, const uint64_t* d_desc,

@@ -24,6 +24,7 @@ LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
 
 
 VAR_NOLB = 8   # launch_info variant bit: the kernel without look-back
+VAR_HOST = 64  # launch_info variant bit: a host path's launch (mapped host memory, host round trip)
 
 
 class QueueBatch(ctypes.Structure):
