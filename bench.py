@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LINK_PEAK_GBPS = 64.0   # PCIe Gen5 x16 per direction, theoretical
 ALLOWED_CPUS = sorted(os.sched_getaffinity(0))   # the process's CPUs, before the host thread is pinned
 EVENT_EVERY = 20  # a kernel-timing sample on timed steps 10, 30, 50, ... (10 samples at K=200)
 EVENT_SPAN = 5    # each sample's HIP event pair brackets 5 consecutive launches
@@ -191,6 +192,9 @@ def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
                            "max": round(rn[-1] / 1e6, 3), "passes": len(rn),
                            "single_core_min_max": [round(r1[0] / 1e6, 3), round(r1[-1] / 1e6, 3)]},
                 "cpus": cpus, "cpus_online": os.cpu_count(), "cpus_in_affinity": len(allowed),
+                "cores_note": (f"{len(cpus)} threads = this job's CPU share on the GPU box (its "
+                               "affinity mask spans the whole machine, whose other cores run other "
+                               "jobs); the GPU's NUMA-local cores first; --cpu-threads N to change"),
                 "cpu_model": model,
                 "sample": sample + "; reference src/worker.c process_packet + TX-flush loop "
                           "(bursts of 32), one shard and calloc'd worker_t per pinned thread"}
@@ -725,8 +729,16 @@ def main() -> None:
                 ("host_mapped_emit", hme, "verdicts + 16-B records written to host memory, frames "
                                           "read only")):
             if h:
+                # the link roofline: the same algorithmic bytes B(p), all of which cross the link
+                # here (descriptor, header extent, verdict, written bytes), per second, against
+                # PCIe Gen5 x16's ~64 GB/s per direction
+                lb = float(algorithmic_bytes(wl, v_first, emit=h["emit"]).sum())
+                link = lb / h["seconds"] / 1e9
                 out[key] = {"value": round(h["packets"] * world / h["seconds"] / 1e6, 2),
                             "unit": "Mpps", "ms_per_batch": round(h["seconds"] * 1e3, 3),
+                            "link": {"achieved": round(link, 2), "peak": LINK_PEAK_GBPS,
+                                     "unit": "GB/s", "frac": round(link / LINK_PEAK_GBPS, 4),
+                                     "algorithmic_bytes_per_packet": round(lb / h["packets"], 2)},
                             "ms_min_max": [round(min(h["times"]) * 1e3, 3),
                                            round(max(h["times"]) * 1e3, 3)],
                             "frame_bytes_in_host_memory": int(wl.frames.nbytes),
