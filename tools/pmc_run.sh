@@ -19,6 +19,8 @@ for g in $groups; do
     ta) ctr="TA_BUSY_avr TA_TA_BUSY_sum" ;;
     tcp) ctr="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" ;;
     tcc) ctr="TCC_HIT_sum TCC_MISS_sum" ;;
+    rdreq) ctr="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" ;;
+    dram) ctr="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum" ;;
   esac
   timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${cfg}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_${mode}_$g.log 2>&1 || echo "pass $g failed rc=$?"
 done
