@@ -307,6 +307,23 @@ int upe_gpu_process_host_emit(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t fram
                               const uint64_t *h_desc, uint32_t *h_verdict, upe_hdr_rec_t *h_hdr,
                               size_t n, size_t chunk, int apply_threads);
 
+/* Egress (reference src/worker.c:240-243, 287-303 and src/tx_afpacket.c:78-118): the forwarded
+ * frames of a classified host batch (verdict code UPE_V_FWD, frames as the path left them —
+ * rewritten in place, or with the emit records applied by upe_hdr_apply), in packet order, handed
+ * to `send` the way the reference's worker loop flushes them: one call per input burst of `burst`
+ * packets that forwarded anything (WORKER_BURST_SIZE = 32 in the reference; at most
+ * UPE_TX_BATCH_MAX = 64 frames per call, the sendmmsg cap of src/tx_afpacket.c:82-84).  `send` has
+ * tx_send_batch's contract with a user pointer first: it returns the frames it sent (negative
+ * counts as 0).  *forwarded += sent and *dropped += count - sent, as the worker counts them
+ * (src/worker.c:290-294); the caller then frees every buffer of the batch.  0, or -1 for a bad
+ * argument (burst 0 or above UPE_TX_BATCH_MAX). */
+#define UPE_TX_BATCH_MAX 64
+typedef int (*upe_tx_batch_fn)(void *user, const uint8_t *const *frames, const size_t *lens,
+                               int count);
+int upe_tx_flush(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t *h_verdict,
+                 size_t n, size_t burst, upe_tx_batch_fn send, void *user, uint64_t *forwarded,
+                 uint64_t *dropped);
+
 /* Pinned (page-locked) host memory for upe_gpu_process_host() batches; the GPU can also read and
  * write it directly (upe_gpu_process_mapped). */
 void *upe_gpu_host_alloc(size_t bytes);

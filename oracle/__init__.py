@@ -83,6 +83,8 @@ def ref_lib() -> ctypes.CDLL:
         lib.upe_refh_process.restype = ctypes.c_int
         lib.upe_refh_process.argtypes = [_P, _SZ, _SZ, ctypes.c_int, _P, _P, _SZ, _P, _SZ, _P,
                                          ctypes.c_uint32, _P, _P, _P, _SZ, _P, _P, _P]
+        lib.upe_refh_tx_log.restype = ctypes.c_int
+        lib.upe_refh_tx_log.argtypes = [_P, _SZ, _P, _SZ, _P, _P]
         lib.upe_refh_time.restype = ctypes.c_double
         lib.upe_refh_time.argtypes = [_P, _SZ, _SZ, _P, _SZ, _P, _SZ, _P, ctypes.c_uint32, _P, _P,
                                       _SZ, ctypes.c_int, _P, ctypes.c_int, _P]
@@ -152,6 +154,20 @@ def run_reference(wl, presorted: bool = False, l1=None) -> Result:
     if rc != 0:
         raise RuntimeError("upe_refh_process failed")
     return Result(frames, verdict, cnt, st, l1, arp, ndp, sorted_out)
+
+
+def tx_log():
+    """The TX calls of the last run_reference on this thread (reference src/worker.c:287-303
+    over the harness's tx_send_batch stub): (sizes per call, packet index of every frame in call
+    order)."""
+    lib = ref_lib()
+    nb, nf = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    lib.upe_refh_tx_log(None, 0, None, 0, ctypes.byref(nb), ctypes.byref(nf))
+    sizes = np.zeros(max(nb.value, 1), np.uint32)
+    frames = np.zeros(max(nf.value, 1), np.uint32)
+    lib.upe_refh_tx_log(_ptr(sizes), sizes.size, _ptr(frames), frames.size, ctypes.byref(nb),
+                        ctypes.byref(nf))
+    return sizes[:nb.value].copy(), frames[:nf.value].copy()
 
 
 def time_reference(wl, threads: int = 1, cpus=None, reps: int = 5, rates=None) -> float:

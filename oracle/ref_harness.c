@@ -37,9 +37,38 @@ int tx_send(const tx_ctx_t *ctx, const uint8_t *frame, size_t len) {
     return 0;
 }
 
+/* The TX log of the last upe_refh_process run on this thread: per tx_send_batch call its frame
+ * count, and per frame the packet index (t_tx_idx maps the worker's tx slots to packet indexes). */
+static __thread size_t t_tx_idx[TX_BATCH_MAX];
+static __thread uint32_t *t_log_sizes, *t_log_frames;
+static __thread size_t t_log_nb, t_log_nf, t_log_cap_b, t_log_cap_f;
+
 int tx_send_batch(const tx_ctx_t *ctx, const uint8_t *const *frames, const size_t *lens, int count) {
     (void)ctx; (void)frames; (void)lens;
+    if (t_log_nb == t_log_cap_b) {
+        t_log_cap_b = t_log_cap_b ? 2 * t_log_cap_b : 1024;
+        t_log_sizes = realloc(t_log_sizes, t_log_cap_b * sizeof(uint32_t));
+    }
+    if (t_log_nf + (size_t)count > t_log_cap_f) {
+        while (t_log_nf + (size_t)count > t_log_cap_f) t_log_cap_f = t_log_cap_f ? 2 * t_log_cap_f : 4096;
+        t_log_frames = realloc(t_log_frames, t_log_cap_f * sizeof(uint32_t));
+    }
+    if (!t_log_sizes || !t_log_frames) return count;
+    t_log_sizes[t_log_nb++] = (uint32_t)count;
+    for (int k = 0; k < count; k++) t_log_frames[t_log_nf++] = (uint32_t)t_tx_idx[k];
     return count;
+}
+
+/* The last run's TX log (upe_refh_process): *nb batches, sizes[0..nb), and the packet index of
+ * every frame handed to tx_send_batch in call order, frames[0..nf).  Either array may be NULL to
+ * ask for the counts. */
+int upe_refh_tx_log(uint32_t *sizes, size_t cap_b, uint32_t *frames, size_t cap_f, size_t *nb,
+                    size_t *nf) {
+    *nb = t_log_nb;
+    *nf = t_log_nf;
+    if (sizes && cap_b >= t_log_nb) memcpy(sizes, t_log_sizes, t_log_nb * sizeof(uint32_t));
+    if (frames && cap_f >= t_log_nf) memcpy(frames, t_log_frames, t_log_nf * sizeof(uint32_t));
+    return 0;
 }
 
 /* The TX flush of worker_main, src/worker.c:286-303. */
@@ -136,6 +165,7 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
     const upe_l1_state_t l1_start = *l1;
     uint8_t orig[PKTBUF_DATA_SIZE];
     int rc = 0;
+    t_log_nb = t_log_nf = 0;
 
     for (size_t base = 0; base < n; base += WORKER_BURST_SIZE) {
         size_t cnt = n - base < WORKER_BURST_SIZE ? n - base : WORKER_BURST_SIZE;
@@ -185,6 +215,7 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
                 counters->arp_reply++;
             }
             uint32_t v;
+            if (w->tx_count != tx0) t_tx_idx[tx0] = i;   /* the TX log's packet index */
             if (w->tx_count != tx0) {
                 v = UPE_V_FWD | (hit ? UPE_VF_NEIGH_HIT : 0) | (l1_init ? UPE_VF_L1_INIT : 0);
             } else if (w->pkts_dropped == d0) {

@@ -122,3 +122,38 @@ def test_egress_list_matches_reference_order(gpu_worker_factory, case, emit):
         want = np.nonzero((ref["verdict"] & 0xF) == code)[0].astype(np.uint32)
         assert want.size > 0 or code != V_FWD or case == "config_a"
         assert np.array_equal(got[code], want), f"code {code}: egress order differs"
+
+
+@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "config_d_small"])
+def test_mapped_batch_to_tx_batches(gpu_worker_factory, case):
+    """The host side end to end: a batch classified in place in pinned host memory
+    (upe_gpu_process_mapped), then cut into TX calls by upe_tx_flush — every call's size, frame
+    order and bytes equal the reference worker's own tx_send_batch calls (src/worker.c:287-303)."""
+    import oracle
+    from upe_amd.layout import desc_lens, desc_offsets
+
+    wl, _ = golden_io.load(case)
+    r = oracle.run_reference(wl)
+    sizes, order = oracle.tx_log()
+    w = gpu_worker_factory(wl.capacity)
+    pf = gpu.PinnedArray(wl.frames.shape, np.uint8)
+    pd = gpu.PinnedArray(wl.desc.shape, np.uint64)
+    pv = gpu.PinnedArray((wl.n,), np.uint32)
+    try:
+        w.configure(wl)
+        pf.array[:] = wl.frames
+        pd.array[:] = wl.desc
+        w.process_mapped(pf.array, pd.array, pv.array)
+        w.sync()
+        batches, fwd, drp = gpu.tx_flush(pf.array, pd.array, pv.array, 32)
+    finally:
+        w.close()
+    assert [len(b[0]) for b in batches] == sizes.tolist()
+    assert np.array_equal(np.concatenate([b[0] for b in batches]), order.astype(np.int64))
+    offs, lens = desc_offsets(wl.desc), desc_lens(wl.desc)
+    for idx, data in batches:
+        for i, d in zip(idx, data):
+            assert d == bytes(r.frames[offs[i]:offs[i] + lens[i]]), f"packet {i} bytes"
+    assert fwd == int(r.counters["pkts_forwarded"][0]) and drp == 0
+    for x in (pf, pd, pv):
+        x.free()

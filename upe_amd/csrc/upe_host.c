@@ -333,3 +333,34 @@ void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec) {
         frame[21] = rec->b[12];
     }
 }
+
+/* ---- egress ------------------------------------------------------------------------------ */
+
+/* The TX side of the worker loop (src/worker.c:240-243 queue, :287-303 flush): per input burst,
+ * the forwarded frames in packet order go to one tx_send_batch-like call. */
+int upe_tx_flush(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t *h_verdict,
+                 size_t n, size_t burst, upe_tx_batch_fn send, void *user, uint64_t *forwarded,
+                 uint64_t *dropped) {
+    if (burst == 0 || burst > UPE_TX_BATCH_MAX)
+        return host_fail("upe_tx_flush: burst %d must be 1..UPE_TX_BATCH_MAX", (int)burst, "");
+    if (n && (!h_frames || !h_desc || !h_verdict || !send))
+        return host_fail("upe_tx_flush: null argument%.0d%s", 0, "");
+    const uint8_t *frames[UPE_TX_BATCH_MAX];
+    size_t lens[UPE_TX_BATCH_MAX];
+    for (size_t base = 0; base < n; base += burst) {
+        const size_t end = n - base < burst ? n : base + burst;
+        int count = 0;
+        for (size_t i = base; i < end; i++) {
+            if (UPE_VERDICT_CODE(h_verdict[i]) != UPE_V_FWD) continue;
+            frames[count] = h_frames + (h_desc[i] >> 16);
+            lens[count++] = (size_t)(h_desc[i] & 0xFFFFu);
+        }
+        if (count == 0) continue;   /* src/worker.c:287: no call for an all-dropped burst */
+        int sent = send(user, frames, lens, count);
+        if (sent < 0) sent = 0;
+        if (sent > count) sent = count;
+        if (forwarded) *forwarded += (uint64_t)sent;
+        if (dropped) *dropped += (uint64_t)(count - sent);
+    }
+    return 0;
+}

@@ -27,6 +27,12 @@ VAR_NOLB = 8   # launch_info variant bit: the kernel without look-back
 VAR_HOST = 64  # launch_info variant bit: a host path's launch (mapped host memory, host round trip)
 
 
+# upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
+TX_BATCH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                               ctypes.c_int)
+
+
 class QueueBatch(ctypes.Structure):
     """upe_gpu_batch_t (include/upe_gpu.h)."""
     _fields_ = [("frames", ctypes.c_void_p), ("desc", ctypes.c_void_p),
@@ -86,6 +92,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_host_unregister": (I, [P]),
         "upe_gpu_process_mapped": (I, [P, P, P, P, SZ, P]),
         "upe_gpu_process_mapped_emit": (I, [P, P, P, P, P, SZ, P]),
+        "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
     }
     sig.update({
         "upe_rules_load_ini": (I, [ctypes.c_char_p, P, SZ, P]),
@@ -121,7 +128,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_rules_load_ini", "upe_pcap_read",
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
-            "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit")
+            "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
+            "upe_tx_flush")
 
 
 def _check(rc: int, what: str) -> None:
@@ -462,6 +470,37 @@ class PinnedArray:
             self.array = None
             LIB.upe_gpu_host_free(self.ptr)
             self.ptr = None
+
+
+def tx_flush(frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray, burst: int = 32,
+             sent_of=None):
+    """upe_tx_flush over a host batch: returns (batches, forwarded, dropped), batches = one
+    (packet indexes, frame bytes) pair per TX call in call order.  sent_of(count) -> frames the
+    stand-in for sendmmsg reports sent (default: all)."""
+    frames = np.ascontiguousarray(frames)
+    desc = np.ascontiguousarray(desc, dtype=np.uint64)
+    verdict = np.ascontiguousarray(verdict, dtype=np.uint32)
+    base = frames.ctypes.data
+    index_of = {int(o): i for i, o in enumerate((desc >> np.uint64(16)).tolist())}
+    batches = []
+
+    def cb(user, fr, lens, count):
+        idx, data = [], []
+        for k in range(count):
+            off = fr[k] - base
+            idx.append(index_of[off])
+            data.append(bytes(frames[off:off + lens[k]]))
+        batches.append((np.array(idx, np.int64), data))
+        return count if sent_of is None else int(sent_of(count))
+
+    fn = TX_BATCH_FN(cb)
+    fwd = ctypes.c_uint64(0)
+    drp = ctypes.c_uint64(0)
+    rc = LIB.upe_tx_flush(_np_ptr(frames), _np_ptr(desc), _np_ptr(verdict), int(desc.shape[0]),
+                          int(burst), fn, None, ctypes.byref(fwd), ctypes.byref(drp))
+    if rc != 0:
+        raise UpeGpuError(f"upe_tx_flush: {LIB.upe_host_last_error().decode()}")
+    return batches, int(fwd.value), int(drp.value)
 
 
 class RegisteredArray:
