@@ -244,7 +244,7 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool, apply_threa
     # last rewritable byte (UPE_REWRITE_EXTENT) plus the verdicts
     lens = desc_lens(src.desc)
     offs = desc_offsets(src.desc)
-    ck = chunk or (1 << 18)
+    ck = chunk or ((1 << 17) if emit else (1 << 18))   # the library's defaults
     h2d = d2h = 0
     for s in range(0, wl.n, ck):
         o, ln = offs[s:s + ck], lens[s:s + ck]
@@ -252,7 +252,7 @@ def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool, apply_threa
         d2h += (20 * len(o) if emit else
                 int((o + np.minimum(ln, REWRITE_EXTENT)).max() - o.min()) + 4 * len(o))
     return {"seconds": t, "packets": wl.n, "h2d_bytes": h2d, "d2h_bytes": d2h,
-            "windows": windows, "chunk": chunk or (1 << 18), "reps": reps,
+            "windows": windows, "chunk": ck, "reps": reps,
             "times": times, "emit": emit, "apply_threads": apply_threads}
 
 

@@ -293,7 +293,7 @@ void upe_hdr_apply(uint8_t *frame, const upe_hdr_rec_t *rec);
 int upe_gpu_process_host(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_bytes,
                          const uint64_t *h_desc, uint32_t *h_verdict, size_t n, size_t chunk);
 
-/* The host round trip in emit mode: the same pipeline, but only the verdicts and the 16-byte
+/* The host round trip in emit mode (chunk 0 = 128k packets): the same pipeline, but only the verdicts and the 16-byte
  * rewritten-header records come back (h_hdr, n records, pinned for the full rate: 20 bytes per
  * packet over the link instead of the frames' rewritten span — the link's two directions share
  * its bandwidth, so fewer bytes back let the frames go in faster).  apply_threads >= 0: the
