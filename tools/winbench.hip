@@ -81,6 +81,9 @@ int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
     const int copies = 16;
     // IMIX sizes 7:4:1, frames back to back at 16-byte alignment, 96 readable bytes after each
+    // layout 0: packed (16-byte aligned); layout 1 (argv[2] = 1): line-aligned, frames of up to 64
+    // bytes on 64-byte boundaries and longer ones on 128-byte boundaries (every window in one line)
+    const int aligned = argc > 2 ? atoi(argv[2]) : 0;
     std::vector<uint64_t> desc(n);
     uint64_t off = 0;
     uint64_t r = 88172645463325252ull;
@@ -88,6 +91,7 @@ int main(int argc, char** argv) {
         r ^= r << 13; r ^= r >> 7; r ^= r << 17;
         const uint32_t k = (uint32_t)(r % 12);
         const uint32_t len = k < 7 ? 64 : k < 11 ? 570 : 1518;
+        if (aligned) off = len <= 64 ? (off + 63) & ~63ull : (off + 127) & ~127ull;
         desc[i] = off << 16 | len;
         off += (len + 15) & ~15u;
     }
@@ -108,8 +112,8 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    printf("winbench: %u IMIX frames, %.1f MB per copy, %d copies, grid %d x %d\n", n,
-           fbytes / 1e6, copies, cus, kBlock);
+    printf("winbench: %u IMIX frames (%s), %.1f MB per copy, %d copies, grid %d x %d\n", n,
+           aligned ? "line-aligned" : "packed", fbytes / 1e6, copies, cus, kBlock);
     for (int mode = 0; mode < 3; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             const int launches = 48;
