@@ -16,6 +16,13 @@ per GPU, each with its own static shard of the packet stream (a full config-B ba
 tables replicated), no data-path collective — weak scaling.  torch.distributed carries only the
 barrier and the max-over-ranks time.
 
+After the timed region (never part of `value`): the other output mode, the IMIX leg, the ring
+leg (16 resident batches per launch), the achievable-bandwidth probe, and the host-inclusive legs
+— the DMA round trip (upe_gpu_process_host[_emit]: pinned hipMemcpyAsync in and out) and the mapped
+path (upe_gpu_process_mapped[_emit]: the kernel reads and writes the pinned host batch over the
+link itself), the latter with a link roofline (the same algorithmic bytes / time against PCIe Gen5
+x16's 64 GB/s).
+
 Prints ONE JSON line (rank 0).  roofline.achieved = algorithmic bytes per launch (SURVEY.md
 §8(d): B(p) = 8 + E(p) + 4 + W(p)) / the mean launch duration, measured with HIP events on the
 launch stream over the timed region (each sample's event pair brackets EVENT_SPAN consecutive
