@@ -193,3 +193,21 @@ def test_mapped_then_resident_carry(gpu_worker_factory):
     finally:
         w.close()
         ref_w.close()
+
+
+@pytest.mark.parametrize("emit", [False, True])
+@pytest.mark.parametrize("n", [1, 63, 65, 1000, 16385])
+def test_mapped_ragged_sizes(gpu_worker_factory, n, emit):
+    """Batch sizes at every edge of the work split (one packet, part of a chunk, a chunk and one,
+    a tile and one), IMIX frames in host memory, against the oracle."""
+    wl = synth.config_c(n=n, seed=900 + n)
+    r = oracle.run_restated(wl)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        _assert_same(_mapped_run(w, wl, emit), {"verdict": r.verdict, "frames": r.frames,
+                                                 "counters": r.counters,
+                                                 "rule_stats": r.rule_stats, "l1": r.l1},
+                     f"mapped n={n} emit={emit}")
+    finally:
+        w.close()
