@@ -296,7 +296,7 @@ def host_mapped(worker, wl, reps: int, emit: bool) -> dict:
 
 
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
-             copies_cap: int) -> dict:
+             copies_cap: int, split: bool = False) -> dict:
     """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
     timed the same way as `value`, on every rank at once after the main region, so that a
     multi-GPU run reports the 64 B and the IMIX rates at each N (BASELINE north_star).  Each rank
@@ -321,16 +321,32 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     base = pool.data_ptr()
+    rbase = rstride = 0
+    if split:
+        # header-split batches: each copy's first-64-byte rows beside its frames
+        rows = torch.from_numpy(synth.header_rows(wl).reshape(-1)).to(dev)
+        rstride = int(rows.numel())
+        rpool = torch.empty(copies * rstride, dtype=torch.uint8, device=dev)
+        for c in range(copies):
+            rpool[c * rstride:(c + 1) * rstride].copy_(rows)
+        del rows
+        rbase = rpool.data_ptr()
 
-    def run(k0: int, count: int, ptrs=None) -> None:
+    def run(k0: int, count: int, ptrs=None, rptrs=None) -> None:
         ptrs = ptrs or [base + (k % copies) * stride for k in range(k0, k0 + count)]
-        if mode == "emit":
+        if split:
+            rptrs = rptrs or [rbase + (k % copies) * rstride for k in range(k0, k0 + count)]
+            worker.process_split_batches_emit(rptrs, ptrs, desc, verdict, hdr, n, sh)
+        elif mode == "emit":
             worker.process_batches_emit(ptrs, desc, verdict, hdr, n, sh)
         else:
             worker.process_batches(ptrs, desc, verdict, n, sh)
 
     timed = gpu.GpuWorker.frames_list([base + (k % copies) * stride
                                        for k in range(warmup, warmup + steps)])
+    rtimed = (gpu.GpuWorker.frames_list([rbase + (k % copies) * rstride
+                                         for k in range(warmup, warmup + steps)])
+              if split else None)
     run(0, warmup)
     torch.cuda.synchronize(dev)
     worker.timing_span(EVENT_EVERY, EVENT_SPAN)
@@ -338,7 +354,7 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run(warmup, steps, timed)
+    run(warmup, steps, timed, rtimed)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -348,7 +364,9 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     cms, _, launches = worker.timing_read()
     worker.close()
     del pool, desc, verdict, hdr
-    bpp = algorithmic_bytes(wl, v, emit=mode == "emit")
+    if split:
+        del rpool
+    bpp = algorithmic_bytes(wl, v, emit=mode == "emit" or split)
     kern_s = cms / launches / 1e3 if launches else float("nan")
     achieved = float(bpp.sum()) / kern_s / 1e9
     return {"workload": WORKLOADS["C"], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
@@ -359,6 +377,9 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                          "kernel_ms": round(kern_s * 1e3, 5),
                          "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
                          "traffic": pmc_traffic("C", n, mode)},
+            "format": ("header-split: each packet's first 64 bytes in a dense row beside the "
+                       "full frames (upe_gpu_process_split_emit)") if split else
+                      "packed frames (upe_gpu_process_emit)",
             "what": f"all ranks at once after the main region, {copies} distinct batch copies "
                     "cycled, same timing protocol as value (barrier, max over ranks)"}
 
@@ -454,6 +475,9 @@ def main() -> None:
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
     ap.add_argument("--imix-copies", type=int, default=32)
+    ap.add_argument("--imix-split", type=int, default=0,
+                    help="1: also time the IMIX leg as header-split batches "
+                         "(upe_gpu_process_split_emit), reported as \"imix_split\"")
     ap.add_argument("--ring", type=int, default=16,
                     help="batches per launch of the ring leg (config B; 0 skips it)")
     args = ap.parse_args()
@@ -596,10 +620,13 @@ def main() -> None:
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
                                     args.workers_per_gpu, args.steps)
-    imix = None
+    imix = imix_split = None
     if args.config == "B" and not args.no_imix and not args.packets:
         imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
                         args.imix_copies)
+        if args.mode == "emit" and args.imix_split:
+            imix_split = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup,
+                                  args.mode, args.imix_copies, split=True)
     ring = None
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
@@ -703,6 +730,8 @@ def main() -> None:
             out["other_mode"] = other
         if imix:
             out["imix"] = imix
+        if imix_split:
+            out["imix_split"] = imix_split
         if ring:
             out["ring"] = ring
         if shared:

@@ -10,6 +10,8 @@
 //      neighbouring lanes take the pieces of one frame (each instruction touches ~13 frames'
 //      lines), staged in LDS (5 KB per wave) and read back per lane
 //   2  per-lane loads of bytes 0..47 only (three pieces; a lower bound)
+//   3  a dense side array of each frame's bytes 0..63 (64-byte stride, four pieces, every line
+//      used whole) plus bytes 64..79 from the frame for the 30 % of frames (IPv6) that need them
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/winbench tools/winbench.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,7 +33,7 @@ constexpr int kBlock = 1024, kWaves = kBlock / 64;
 
 template <int kMode>
 __global__ void __launch_bounds__(kBlock) win(const uint8_t* frames, const uint64_t* desc,
-                                              uint32_t* out, uint32_t n) {
+                                              uint32_t* out, uint32_t n, const uint4* side) {
     __shared__ uint4 stage[kMode == 1 ? kWaves * 320 : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t nch = (n + 63) / 64;
@@ -57,6 +59,12 @@ __global__ void __launch_bounds__(kBlock) win(const uint8_t* frames, const uint6
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             for (int c = 0; c < 5; ++c) w[c] = st[5 * lane + c];
             __builtin_amdgcn_wave_barrier();
+        } else if (kMode == 3 && live) {
+            const uint64_t dsc = desc[i];
+            const uint32_t len = (uint32_t)(dsc & 0xFFFF);
+            for (int c = 0; c < 4; ++c) w[c] = side[4 * (size_t)i + c];
+            if (len > 64u && (i * 2654435761u) % 10u < 3u)   // the IPv6 share
+                w[4] = reinterpret_cast<const uint4*>(frames + (dsc >> 16))[4];
         } else if (live) {
             const uint64_t dsc = desc[i];
             const uint32_t len = (uint32_t)(dsc & 0xFFFF);
@@ -114,15 +122,22 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     printf("winbench: %u IMIX frames (%s), %.1f MB per copy, %d copies, grid %d x %d\n", n,
            aligned ? "line-aligned" : "packed", fbytes / 1e6, copies, cus, kBlock);
-    for (int mode = 0; mode < 3; ++mode) {
+    uint4* side;
+    CK(hipMalloc(&side, (size_t)n * 64 * copies));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(side),
+                       (size_t)n * 16 * copies);
+    CK(hipDeviceSynchronize());
+    for (int mode = 0; mode < 4; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             const int launches = 48;
             CK(hipEventRecord(e0));
             for (int k = 0; k < launches; ++k) {
                 const uint8_t* f = frames + (size_t)(k % copies) * stride;
-                if (mode == 0) hipLaunchKernelGGL(win<0>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n);
-                if (mode == 1) hipLaunchKernelGGL(win<1>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n);
-                if (mode == 2) hipLaunchKernelGGL(win<2>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n);
+                const uint4* sd = side + (size_t)(k % copies) * n * 4;
+                if (mode == 0) hipLaunchKernelGGL(win<0>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n, sd);
+                if (mode == 1) hipLaunchKernelGGL(win<1>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n, sd);
+                if (mode == 2) hipLaunchKernelGGL(win<2>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n, sd);
+                if (mode == 3) hipLaunchKernelGGL(win<3>, dim3(cus), dim3(kBlock), 0, 0, f, d_desc, out, n, sd);
             }
             CK(hipGetLastError());
             CK(hipEventRecord(e1));

@@ -381,6 +381,9 @@ struct Args {
     // launch is resident before any of the next, so the next one's wait always ends)
     uint32_t fin_flags, fin_wait, start_target;
     unsigned long long* sig;
+    // header-split batch (upe_gpu_process_split_emit): bytes 0..63 of packet i at slab[4 i ..
+    // 4 i + 3] (zero past len); bytes 64.. from the frame.  nullptr: every byte from the frame.
+    const uint4* slab;
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2].s; }
@@ -1208,7 +1211,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kQueue = false, bool kHost = false>
+          bool kQueue = false, bool kHost = false, bool kSplit = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1241,16 +1244,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past len
     // are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame costs
     // four loads, not five.  Frames shorter than 49 bytes never take the fast path.
-    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[20]) {
+    // (A header-split batch, a.slab: bytes 0..63 as one dense 64-byte row per packet — whole
+    // lines, coalesced across the wave — and bytes 64..79 from the frame when it has them.)
+    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[20], uint32_t pi) {
 #pragma unroll
         for (int j = 0; j < 20; ++j) w[j] = 0;
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
+            const uint4* h = kSplit ? a.slab + 4 * (size_t)pi : q;
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
                 if (c < 3 || len > 16u * c) {
-                    const uint4 v = ldf<kHost>(&q[c]);
+                    const uint4 v = ldf<kHost>(c < 4 ? &h[c] : &q[c]);
                     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
                 }
             }
@@ -1263,15 +1269,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     constexpr bool kMid = (UPE_MID_PREFETCH & 1) && (!kTssMode || (UPE_MID_PREFETCH & 4)) &&
                           (kEmit || (UPE_MID_PREFETCH & 2));
     struct Win { uint4 c0, c1, c2, c3, c4; };
-    auto fetch_window = [&](uint64_t dsc, bool live) -> Win {
+    auto fetch_window = [&](uint64_t dsc, bool live, uint32_t pi) -> Win {
         const uint4 z = make_uint4(0, 0, 0, 0);
         Win v{z, z, z, z, z};
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            v.c0 = ldf<kHost>(&q[0]); v.c1 = ldf<kHost>(&q[1]); v.c2 = ldf<kHost>(&q[2]);
+            const uint4* h = kSplit ? a.slab + 4 * (size_t)pi : q;
+            v.c0 = ldf<kHost>(&h[0]); v.c1 = ldf<kHost>(&h[1]); v.c2 = ldf<kHost>(&h[2]);
             if (!kWin48) {
-                if (len > 48u) v.c3 = ldf<kHost>(&q[3]);
+                if (len > 48u) v.c3 = ldf<kHost>(&h[3]);
                 if (len > 64u) v.c4 = ldf<kHost>(&q[4]);
             }
         }
@@ -1499,7 +1506,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 w[4 * j + 0] = c[j].x; w[4 * j + 1] = c[j].y; w[4 * j + 2] = c[j].z; w[4 * j + 3] = c[j].w;
             }
         } else {
-            load_window(dsc, live, w);
+            load_window(dsc, live, w, i);
         }
         have_nw = false;
         dsc_next = 0;
@@ -1616,7 +1623,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // the next chunk's window (its descriptor has been back since early in this chunk):
         // issued here, it arrives while this chunk finishes
         if (kMid && chn != kNone) {
-            nw = fetch_window(dsc_next, chn * 64u + (uint32_t)lane < a.n);
+            nw = fetch_window(dsc_next, chn * 64u + (uint32_t)lane < a.n, chn * 64u + (uint32_t)lane);
             have_nw = true;
         }
 
@@ -2537,47 +2544,43 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 128;
+constexpr int kVarCount = 256;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 queue (overlapped launches; emit only), bit 6
-// a host path's launch (upe_gpu_process_mapped / upe_gpu_process_host; not ring or queue).
+// a host path's launch (upe_gpu_process_mapped / upe_gpu_process_host; not ring or queue), bit 7
+// a header-split batch (upe_gpu_process_split_emit; emit only, not ring, queue or host).
 int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool queue = false,
-                 bool host = false) {
-    return (host && !ring && !queue ? 64 : 0) | (queue && emit ? 32 : 0) | (ring ? 16 : 0) |
+                 bool host = false, bool split = false) {
+    return (split && emit && !ring && !queue && !host ? 128 : 0) |
+           (host && !ring && !queue ? 64 : 0) | (queue && emit ? 32 : 0) | (ring ? 16 : 0) |
            (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+}
+// The instantiated variants (every combination classify_var can return for a launch).
+constexpr bool var_built(int v) {
+    const bool emit = v & 1, lean = v & 4, nolb = v & 8, ring = v & 16, queue = v & 32,
+               host = v & 64, split = v & 128;
+    if (nolb && !lean) return false;
+    if (ring) return !split && !queue && !host && emit && lean && !(v & 2);
+    if (queue) return !split && !host && emit;
+    if (split) return emit && !host;
+    return true;
 }
 template <int V>
 const void* classify_fn_of() {
-    return reinterpret_cast<const void*>(
-        &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0,
-                      (V & 32) != 0, (V & 64) != 0>);
+    if constexpr (var_built(V))
+        return reinterpret_cast<const void*>(
+            &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0,
+                          (V & 32) != 0, (V & 64) != 0, (V & 128) != 0>);
+    else
+        return nullptr;
+}
+template <int... V>
+constexpr std::array<const void* (*)(), sizeof...(V)> classify_table(std::integer_sequence<int, V...>) {
+    return {{&classify_fn_of<V>...}};
 }
 const void* classify_fn(int var) {
-    static const void* const fns[kVarCount] = {
-        classify_fn_of<0>(), classify_fn_of<1>(), classify_fn_of<2>(), classify_fn_of<3>(),
-        classify_fn_of<4>(), classify_fn_of<5>(), classify_fn_of<6>(), classify_fn_of<7>(),
-        nullptr, nullptr, nullptr, nullptr,
-        classify_fn_of<12>(), classify_fn_of<13>(), classify_fn_of<14>(), classify_fn_of<15>(),
-        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<21>(), nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<29>(), nullptr, nullptr,
-        // queue variants (emit)
-        nullptr, classify_fn_of<33>(), nullptr, classify_fn_of<35>(),
-        nullptr, classify_fn_of<37>(), nullptr, classify_fn_of<39>(),
-        nullptr, nullptr, nullptr, nullptr, nullptr, classify_fn_of<45>(), nullptr, classify_fn_of<47>(),
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        // host-memory variants (upe_gpu_process_mapped[_emit])
-        classify_fn_of<64>(), classify_fn_of<65>(), classify_fn_of<66>(), classify_fn_of<67>(),
-        classify_fn_of<68>(), classify_fn_of<69>(), classify_fn_of<70>(), classify_fn_of<71>(),
-        nullptr, nullptr, nullptr, nullptr,
-        classify_fn_of<76>(), classify_fn_of<77>(), classify_fn_of<78>(), classify_fn_of<79>(),
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    return var >= 0 && var < kVarCount ? fns[var] : nullptr;
+    static const auto fns = classify_table(std::make_integer_sequence<int, kVarCount>{});
+    return var >= 0 && var < kVarCount ? fns[var]() : nullptr;
 }
 
 void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Args& a) {
@@ -2599,8 +2602,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
 // The persistent grid of a kernel configuration: the occupancy API's answer, checked by a census
 // launch the first time the configuration is used (census_probe).  0 on error.
 uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
-    static_assert(kVarCount <= 128, "the variant takes the key's low 7 bits");
-    const uint64_t key = (uint64_t)lds << 7 | (uint64_t)var;
+    static_assert(kVarCount <= 256, "the variant takes the key's low 8 bits");
+    const uint64_t key = (uint64_t)lds << 8 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
     // a census counts what an idle chip holds: let an overlapped queue's previous launch finish
@@ -3298,7 +3301,7 @@ struct RingReq {
 };
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
-                 const RingReq* ring = nullptr, bool host = false) {
+                 const RingReq* ring = nullptr, bool host = false, const uint4* slab = nullptr) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
@@ -3312,7 +3315,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             const size_t m = n - s0 < kMaxLaunch ? n - s0 : kMaxLaunch;
             if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
                              d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
-                             m, stream, nullptr, host) != 0)
+                             m, stream, nullptr, host, slab ? slab + 4 * s0 : nullptr) != 0)
                 return -1;
         }
         return 0;
@@ -3379,6 +3382,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.stats_idx = c->stats_idx;
     a.flow_hash = d_flow_hash;
     a.hdr = reinterpret_cast<uint4*>(d_hdr);
+    a.slab = slab;
     const bool emit = d_hdr != nullptr && n > 0;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     a.lens16 = nullptr;
@@ -3433,14 +3437,15 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     bool stamp = ring && ring->done && emit && lean && !c->tss;
     const bool queue = c->fin_next_flags != 0;   // a launch of upe_gpu_process_queue_emit
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue, host);
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue, host, slab != nullptr);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue, host), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue, host,
+                                      slab != nullptr), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3551,6 +3556,29 @@ int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_
                          uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (n && !d_hdr) return fail("null header records");
     return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
+}
+
+int upe_gpu_process_split_emit(upe_gpu_ctx_t* c, const uint8_t* d_hdrs, uint8_t* d_frames,
+                               const uint64_t* d_desc, uint32_t* d_verdict, upe_hdr_rec_t* d_hdr,
+                               size_t n, void* stream) {
+    if (n && !d_hdr) return fail("null header records");
+    if (n && !d_hdrs) return fail("null header rows");
+    if (((uintptr_t)d_hdrs & 15u) != 0) return fail("header rows must be 16-byte aligned");
+    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream, nullptr, false,
+                        reinterpret_cast<const uint4*>(d_hdrs));
+}
+
+int upe_gpu_process_split_batches_emit(upe_gpu_ctx_t* c, const uint8_t* const* d_hdrs_list,
+                                       uint8_t* const* d_frames_list, const uint64_t* d_desc,
+                                       uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n,
+                                       size_t count, void* stream) {
+    if (!c) return fail("null context");
+    if (count && (!d_hdrs_list || !d_frames_list)) return fail("null batch list");
+    for (size_t k = 0; k < count; ++k)
+        if (upe_gpu_process_split_emit(c, d_hdrs_list[k], d_frames_list[k], d_desc, d_verdict,
+                                       d_hdr, n, stream) != 0)
+            return -1;
+    return 0;
 }
 
 int upe_gpu_process_ring_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
