@@ -376,7 +376,7 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "kernel_ms": round(kern_s * 1e3, 5),
                          "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
-                         "traffic": pmc_traffic("C", n, mode)},
+                         "traffic": None if split else pmc_traffic("C", n, mode)},
             "format": ("header-split: each packet's first 64 bytes in a dense row beside the "
                        "full frames (upe_gpu_process_split_emit)") if split else
                       "packed frames (upe_gpu_process_emit)",
@@ -475,7 +475,7 @@ def main() -> None:
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
     ap.add_argument("--imix-copies", type=int, default=32)
-    ap.add_argument("--imix-split", type=int, default=0,
+    ap.add_argument("--imix-split", type=int, default=1,
                     help="1: also time the IMIX leg as header-split batches "
                          "(upe_gpu_process_split_emit), reported as \"imix_split\"")
     ap.add_argument("--ring", type=int, default=16,
