@@ -713,16 +713,26 @@ __global__ void upe_l1_sync(DevL1* l1, BatchAcc* acc, const TilePay* pay) {
 // Small tables are read from an LDS copy (staged at kernel entry, broadcast reads of a
 // wave-uniform address: no scalar-cache round trip in the dependent chain); larger ones through
 // the scalar unit from the constant address space.
+// UPE_RULE_PREFIX=1 (measured, off): larger tables get their first kSmallRules rules staged in
+// LDS too, scanned from there before the rest goes through the scalar unit, so a wave whose
+// packets all match early (config C: every wave within its first 12 rules) waits on no scalar
+// load.  Parity-green, but B 43.5-43.6 vs 43.8-44.1 Gpps and C 39.55 vs 39.3 us per batch
+// (profiles/r03/v8_rule_prefix_ab.txt): C's rule words already hit in the scalar cache.
+#ifndef UPE_RULE_PREFIX
+#define UPE_RULE_PREFIX 0
+#endif
+constexpr bool kRulePrefix = UPE_RULE_PREFIX;
 template <bool V6, bool kLdsRules>
 __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4],
                                                const uint32_t d[4], uint32_t& act,
-                                               const u32x8* l4, const u32x16* l6) {
+                                               const u32x8* l4, const u32x16* l6,
+                                               uint32_t b0, uint32_t b1) {
     uint32_t hit = kNone;
     static_assert(sizeof(RuleV4) == 32 && sizeof(RuleV6) == 64, "rule stream strides");
     const auto* rv4 = as_const<u32x8>(a.rv4);
     const auto* rv6 = as_const<u32x16>(a.rv6);
-    for (uint32_t b = 0; b < a.nrules_pad; b += kUnroll) {
+    for (uint32_t b = b0; b < b1; b += kUnroll) {
         // the rule index is wave-uniform: say so, so rule words come through the scalar unit
         const uint32_t base = __builtin_amdgcn_readfirstlane(b);
 #pragma unroll
@@ -1325,13 +1335,15 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
     uint64_t dsc_next = 0;
     if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[ch * 64u + lane]);
-    if (!kTssMode && small_stats) {
+    if (!kTssMode && (small_stats || kRulePrefix)) {
+        // the whole table (small tables) or its first kSmallRules rules (the scan's LDS prefix)
+        const uint32_t nst = a.nrules_pad < (uint32_t)kSmallRules ? a.nrules_pad : (uint32_t)kSmallRules;
         const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
         const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
         uint4* d4 = reinterpret_cast<uint4*>(s_rv4);
         uint4* d6 = reinterpret_cast<uint4*>(s_rv6);
-        for (uint32_t k = tid; k < 2 * a.nrules_pad; k += kBlock) d4[k] = g4[k];
-        for (uint32_t k = tid; k < 4 * a.nrules_pad; k += kBlock) d6[k] = g6[k];
+        for (uint32_t k = tid; k < 2 * nst; k += kBlock) d4[k] = g4[k];
+        for (uint32_t k = tid; k < 4 * nst; k += kBlock) d6[k] = g6[k];
     }
     // The starting L1 entries: the state after batch k - 2 (one scalar load) with batch k - 1's
     // outcome folded in (its replicated minima / maxima, then at most two payload loads).
@@ -1593,12 +1605,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else if (kTssMode) {
             ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act, s_fps);
         } else {
-            if (small_stats)
-                ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
-                             : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6);
-            else
-                ri = need_v6 ? scan_rules<true, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6)
-                             : scan_rules<false, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6);
+            // small tables: all in LDS; larger ones: the LDS-staged first kSmallRules rules, then
+            // (only while some lane is unmatched) the rest through the scalar unit
+            const uint32_t nl = small_stats ? a.nrules_pad
+                                            : (kRulePrefix ? (uint32_t)kSmallRules : 0u);
+            ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nl)
+                         : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nl);
+            if (!small_stats && __any(ok && ri == kNone)) {
+                const bool fin = !ok || ri != kNone;   // matched lanes take no later rule
+                const uint32_t r2 =
+                    need_v6 ? scan_rules<true, false>(a, fin, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, nl, a.nrules_pad)
+                            : scan_rules<false, false>(a, fin, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, nl, a.nrules_pad);
+                if (ri == kNone) ri = r2;
+            }
         }
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
