@@ -202,6 +202,18 @@ void upe_gpu_close(upe_gpu_ctx_t *ctx);
  * w->rt (src/worker.c:129).  count <= rule capacity given at open, every rule_id < capacity. */
 int upe_gpu_load_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count);
 
+/* Rule reload with the reference's SIGHUP semantics (src/main.c:216-282: a new table, a fresh
+ * calloc'd rule_stats of the new table's capacity per worker, w->rt and w->rule_stats swapped
+ * between two bursts; pkts_* and the L1 neighbour caches untouched).  The batches queued so far
+ * finish with the old table; if old_stats is given, rule_stats[0..old_capacity) as they stand
+ * then (indexed by the OLD table's rule_ids, what the stats thread last printed) are copied out
+ * — the reference frees them after its grace period.  The next batch runs with rules[0..count)
+ * (sorted, as for upe_gpu_load_rules; rule_id < rule_capacity) and rule_stats all zero, sized
+ * rule_capacity (upe_gpu_get_stats reads that many from now on).  Counters and the L1 state
+ * carry on.  Arguments are checked before anything changes.  Synchronous; 0 / -1. */
+int upe_gpu_reload_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count,
+                         size_t rule_capacity, upe_rule_stat_t *old_stats, size_t old_capacity);
+
 /* How the loaded table is classified: 0 = linear first-match scan (small tables, or many mask
  * signatures), 1 = tuple-space index (large tables whose rules fall into few mask signatures:
  * one hash probe per signature, visited in order of each signature's first rule, so the result
@@ -395,21 +407,11 @@ typedef struct upe_gpu_batch {
 } upe_gpu_batch_t;
 
 /* The worker loop (reference src/worker.c:255-307: burst after burst, the worker's state carried
- * from one to the next) over `count` resident batches in emit mode, one launch per batch, with
- * consecutive launches overlapped: launch k + 1 goes to a second stream and is dispatched once
- * every workgroup of launch k is resident (a stream wait on a signal word launch k's last
- * workgroup to start writes), so its workgroups take CUs as launch k's finish, stage their
- * tables and then wait inside the kernel for launch k's finished-workgroup count before they
- * read the state it leaves.  The kernel-boundary gap and the next batch's prologue are hidden
- * behind the previous batch's tail.  Results — every verdict, record, counter, rule_stats word
- * and the L1 state — equal `count` upe_gpu_process_emit() calls in order; batches may share
- * descriptor and output buffers (each batch's stores come after the previous batch's finished).
- * Falls back to sequential launches for tables of more than 4096 rules (their rule_stats
- * group-by follows each launch) or batches over 2^24 packets.  The overlap is opt-in
- * (environment UPE_GPU_OVERLAP=1): on MI355X it measured slower than one launch after another
- * (config B 25.2 vs 24.2 us per batch, C 45 vs 39), so by default the batches run
- * as sequential upe_gpu_process_emit() launches.  `stream` orders the queue after earlier work
- * and everything after it.  0 / -1. */
+ * from one to the next) over `count` resident batches in emit mode, one launch per batch queued
+ * from native code on `stream`.  Results — every verdict, record, counter, rule_stats word and
+ * the L1 state — equal `count` upe_gpu_process_emit() calls in order; batches may differ in size
+ * (an empty one is a no-op) and may share descriptor and output buffers.  Every batch is
+ * checked (a batch of n > 0 packets needs its records) before any is queued.  0 / -1. */
 int upe_gpu_process_queue_emit(upe_gpu_ctx_t *ctx, const upe_gpu_batch_t *batches, size_t count,
                                void *stream);
 
@@ -459,12 +461,11 @@ int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
  * defers them, and the launch's last workgroup answers them. */
 typedef struct {
     uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back,
-                          4 ring, 5 queue, 6 a host path (upe_gpu_process_mapped / _host) */
+                          4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host),
+                          6 a header-split batch */
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */
-    uint32_t overlapped; /* launches so far that ran overlapped with their predecessor
-                            (upe_gpu_process_queue_emit) */
     uint64_t launches; /* classify launches of this context so far */
 } upe_launch_info_t;
 int upe_gpu_launch_info(upe_gpu_ctx_t *ctx, upe_launch_info_t *info);

@@ -83,6 +83,10 @@ def ref_lib() -> ctypes.CDLL:
         lib.upe_refh_process.restype = ctypes.c_int
         lib.upe_refh_process.argtypes = [_P, _SZ, _SZ, ctypes.c_int, _P, _P, _SZ, _P, _SZ, _P,
                                          ctypes.c_uint32, _P, _P, _P, _SZ, _P, _P, _P]
+        lib.upe_refh_process_reload.restype = ctypes.c_int
+        lib.upe_refh_process_reload.argtypes = [_P, _SZ, _SZ, _P, _SZ, _SZ, _P, _SZ, _P, _SZ, _P,
+                                                _SZ, _P, ctypes.c_uint32, _P, _P, _P, _SZ, _P, _P,
+                                                _P, _P]
         lib.upe_refh_tx_log.restype = ctypes.c_int
         lib.upe_refh_tx_log.argtypes = [_P, _SZ, _P, _SZ, _P, _P]
         lib.upe_refh_time.restype = ctypes.c_double
@@ -154,6 +158,33 @@ def run_reference(wl, presorted: bool = False, l1=None) -> Result:
     if rc != 0:
         raise RuntimeError("upe_refh_process failed")
     return Result(frames, verdict, cnt, st, l1, arp, ndp, sorted_out)
+
+
+def run_reference_reload(wl, rules_b, capacity_b: int, at: int, l1=None):
+    """The reference worker with the stats thread's SIGHUP reload (src/main.c:216-282) between
+    packets at-1 and at: table A = wl.rules (insertion order), then table B = rules_b (insertion
+    order) with a fresh rule_stats[capacity_b].  Returns (Result with rule_stats = the new array
+    and rules_sorted = table B as built, the old array as it stood at the swap)."""
+    lib = ref_lib()
+    ra = np.ascontiguousarray(wl.rules, dtype=RULE_DTYPE)
+    rb = np.ascontiguousarray(rules_b, dtype=RULE_DTYPE)
+    sorted_b = np.zeros(len(rb), RULE_DTYPE)
+    frames = wl.frames.copy()
+    arp = wl.arp.copy()
+    ndp = wl.ndp.copy()
+    l1 = (wl.l1 if l1 is None else l1).copy()
+    verdict = np.zeros(wl.n, dtype=np.uint32)
+    cnt = np.zeros(1, COUNTERS_DTYPE)
+    st_a = np.zeros(wl.capacity, RULE_STAT_DTYPE)
+    st_b = np.zeros(capacity_b, RULE_STAT_DTYPE)
+    eth = _eth(wl)
+    rc = lib.upe_refh_process_reload(_ptr(ra), len(ra), wl.capacity, _ptr(rb), len(rb), capacity_b,
+                                     _ptr(sorted_b), at, _ptr(arp), len(arp), _ptr(ndp), len(ndp),
+                                     _ptr(eth), wl.ip4_addr, _ptr(l1), _ptr(frames), _ptr(wl.desc),
+                                     wl.n, _ptr(verdict), _ptr(cnt), _ptr(st_a), _ptr(st_b))
+    if rc != 0:
+        raise RuntimeError("upe_refh_process_reload failed")
+    return Result(frames, verdict, cnt, st_b, l1, arp, ndp, sorted_b), st_a
 
 
 def tx_log():

@@ -113,68 +113,27 @@ static void get_l1(const worker_t *w, upe_l1_state_t *l1) {
     memcpy(l1->last_ndp_mac, w->last_ndp_mac, 6);
 }
 
-/*
- * Process a batch (include/upe_gpu.h "Batch layout") through the reference worker.
- * rules: insertion order (rule_table_add assigns rule_id and sorts) unless presorted.
- * sorted_out (optional): rt->rules after the build.
- * arp/ndp: slot arrays, updated in place by control packets exactly as the reference does.
- * l1, counters, rule_stats[capacity]: in/out, accumulate.
- */
-int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, int presorted,
-                     upe_rule_t *sorted_out, upe_arp_entry_t *arp, size_t arp_cap,
-                     upe_ndp_entry_t *ndp, size_t ndp_cap, const uint8_t eth_addr[6],
-                     uint32_t ip4_addr, upe_l1_state_t *l1, uint8_t *frames, const uint64_t *desc,
-                     size_t n, uint32_t *verdict, upe_counters_t *counters,
-                     upe_rule_stat_t *rule_stats) {
-    rule_table_t rt;
-    if (build_rules(&rt, rules, nrules, capacity, presorted) != 0) return -1;
-    if (sorted_out) memcpy(sorted_out, rt.rules, rt.count * sizeof(rule_t));
+/* One pass of worker_main's burst loop (src/worker.c:267-303, minus the ring pop) over packets
+ * [i0, i1): bursts of WORKER_BURST_SIZE, process_packet on each packet with the worker's current
+ * w->rt, then the TX flush; the verdict word of each packet read back from what process_packet
+ * observably did (file header). */
+static pktbuf_pool_t g_pool;
+static int g_pool_ready;
 
-    arp_table_t arpt;
-    ndp_table_t ndpt;
-    size_t acap = arp_cap ? arp_cap : 1, ncap = ndp_cap ? ndp_cap : 1;
-    if (arp_table_init(&arpt, acap) != 0 || ndp_table_init(&ndpt, ncap) != 0) return -1;
-    if (arp_cap) memcpy(arpt.entries, arp, arp_cap * sizeof(arp_entry_t));
-    if (ndp_cap) memcpy(ndpt.entries, ndp, ndp_cap * sizeof(ndp_entry_t));
-
-    tx_ctx_t tx;
-    memset(&tx, 0, sizeof tx);
-    memcpy(tx.eth_addr, eth_addr, 6);
-    tx.ip4_addr = ip4_addr;
-
-    /* One pool for the process lifetime: pktbuf.c's thread-local cache remembers the pool by
-     * address (src/pktbuf.c:298-303), so a destroyed pool must never be followed by a new one
-     * on the same thread. */
-    static pktbuf_pool_t pool;
-    static int pool_ready;
-    if (!pool_ready) {
-        if (pktbuf_pool_init(&pool, 256) != 0) return -1;
-        pool_ready = 1;
-    }
-
-    worker_t *w = calloc(1, sizeof(worker_t));
-    if (!w || worker_init(w, 0, -1, NULL, &pool, &rt, &tx, &arpt, &ndpt) != 0) return -1;
-    put_l1(w, l1);
-    if (rule_stats) memcpy(w->rule_stats, rule_stats, capacity * sizeof(rule_stat_t));
-    w->pkts_in = counters->pkts_in;
-    w->pkts_parsed = counters->pkts_parsed;
-    w->pkts_matched = counters->pkts_matched;
-    w->pkts_forwarded = counters->pkts_forwarded;
-    w->pkts_dropped = counters->pkts_dropped;
-
-    const upe_l1_state_t l1_start = *l1;
+static int run_range(worker_t *w, const upe_l1_state_t *l1_start, uint8_t *frames,
+                     const uint64_t *desc, size_t i0, size_t i1, uint32_t *verdict,
+                     upe_counters_t *counters) {
+    const rule_table_t *rt = w->rt;
     uint8_t orig[PKTBUF_DATA_SIZE];
     int rc = 0;
-    t_log_nb = t_log_nf = 0;
-
-    for (size_t base = 0; base < n; base += WORKER_BURST_SIZE) {
-        size_t cnt = n - base < WORKER_BURST_SIZE ? n - base : WORKER_BURST_SIZE;
+    for (size_t base = i0; base < i1; base += WORKER_BURST_SIZE) {
+        size_t cnt = i1 - base < WORKER_BURST_SIZE ? i1 - base : WORKER_BURST_SIZE;
         w->pkts_in += cnt; /* src/worker.c:280 */
         for (size_t j = 0; j < cnt; j++) {
             size_t i = base + j;
             size_t off = (size_t)(desc[i] >> 16), len = (size_t)(desc[i] & 0xFFFF);
             if (len > PKTBUF_DATA_SIZE) { rc = -1; len = PKTBUF_DATA_SIZE; }
-            pktbuf_t *b = pktbuf_alloc(&pool);
+            pktbuf_t *b = pktbuf_alloc(&g_pool);
             if (!b) return -1;
             memset(b->data, 0, PKTBUF_DATA_SIZE);
             memcpy(b->data, frames + off, len);
@@ -199,13 +158,13 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
             if (parsed && key.ip_ver == 4) {
                 uint8_t mac[6];
                 hit = (w->last_arp_ip != 0 && key.dst_ip.v4 == w->last_arp_ip) ||
-                      arp_get_mac(&arpt, key.dst_ip.v4, mac);
-                l1_init = l1_start.last_arp_ip != 0 && key.dst_ip.v4 == l1_start.last_arp_ip;
+                      arp_get_mac(w->arpt, key.dst_ip.v4, mac);
+                l1_init = l1_start->last_arp_ip != 0 && key.dst_ip.v4 == l1_start->last_arp_ip;
             } else if (parsed && key.ip_ver == 6) {
                 uint8_t mac[6];
                 hit = memcmp(key.dst_ip.v6, w->last_ndp_ip, 16) == 0 ||
-                      ndp_get_mac(&ndpt, key.dst_ip.v6, mac);
-                l1_init = memcmp(key.dst_ip.v6, l1_start.last_ndp_ip, 16) == 0;
+                      ndp_get_mac(w->ndpt, key.dst_ip.v6, mac);
+                l1_init = memcmp(key.dst_ip.v6, l1_start->last_ndp_ip, 16) == 0;
             }
 
             process_packet(w, b);
@@ -226,14 +185,14 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
             } else if (w->pkts_matched == m0) {
                 v = UPE_V_DROP_NOMATCH;
             } else {
-                const rule_t *r = rule_table_match(&rt, &key);
+                const rule_t *r = rule_table_match(rt, &key);
                 v = r->action.type == ACT_DROP  ? UPE_V_DROP_RULE
                     : r->action.type == ACT_FWD ? UPE_V_DROP_TTL
                                                 : UPE_V_DROP_ACTION;
             }
             if (w->pkts_matched != m0) {
-                const rule_t *r = rule_table_match(&rt, &key);
-                v |= (uint32_t)(r - rt.rules + 1) << 8;
+                const rule_t *r = rule_table_match(rt, &key);
+                v |= (uint32_t)(r - rt->rules + 1) << 8;
             }
             verdict[i] = v | flags;
             size_t wb = len < 64 ? len : 64;
@@ -241,22 +200,150 @@ int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, in
         }
         flush_tx(w);
     }
+    return rc;
+}
 
+/* A calloc'd worker_t (src/main.c:444) over the given tables, with the caller's L1 state,
+ * counters and rule_stats[capacity]. */
+static worker_t *new_worker(const rule_table_t *rt, const tx_ctx_t *tx, arp_table_t *arpt,
+                            ndp_table_t *ndpt, const upe_l1_state_t *l1,
+                            const upe_counters_t *counters, const upe_rule_stat_t *rule_stats,
+                            size_t capacity) {
+    /* One pool for the process lifetime: pktbuf.c's thread-local cache remembers the pool by
+     * address (src/pktbuf.c:298-303), so a destroyed pool must never be followed by a new one
+     * on the same thread. */
+    if (!g_pool_ready) {
+        if (pktbuf_pool_init(&g_pool, 256) != 0) return NULL;
+        g_pool_ready = 1;
+    }
+    worker_t *w = calloc(1, sizeof(worker_t));
+    if (!w || worker_init(w, 0, -1, NULL, &g_pool, rt, tx, arpt, ndpt) != 0) return NULL;
+    put_l1(w, l1);
+    if (rule_stats) memcpy(w->rule_stats, rule_stats, capacity * sizeof(rule_stat_t));
+    w->pkts_in = counters->pkts_in;
+    w->pkts_parsed = counters->pkts_parsed;
+    w->pkts_matched = counters->pkts_matched;
+    w->pkts_forwarded = counters->pkts_forwarded;
+    w->pkts_dropped = counters->pkts_dropped;
+    return w;
+}
+
+static void worker_out(const worker_t *w, upe_l1_state_t *l1, upe_counters_t *counters) {
     get_l1(w, l1);
     counters->pkts_in = w->pkts_in;
     counters->pkts_parsed = w->pkts_parsed;
     counters->pkts_matched = w->pkts_matched;
     counters->pkts_forwarded = w->pkts_forwarded;
     counters->pkts_dropped = w->pkts_dropped;
-    if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
-    if (arp_cap) memcpy(arp, arpt.entries, arp_cap * sizeof(arp_entry_t));
-    if (ndp_cap) memcpy(ndp, ndpt.entries, ndp_cap * sizeof(ndp_entry_t));
+}
 
+typedef struct {
+    arp_table_t arpt;
+    ndp_table_t ndpt;
+    tx_ctx_t tx;
+} env_t;
+
+static int env_init(env_t *e, const upe_arp_entry_t *arp, size_t arp_cap,
+                    const upe_ndp_entry_t *ndp, size_t ndp_cap, const uint8_t eth_addr[6],
+                    uint32_t ip4_addr) {
+    size_t acap = arp_cap ? arp_cap : 1, ncap = ndp_cap ? ndp_cap : 1;
+    if (arp_table_init(&e->arpt, acap) != 0 || ndp_table_init(&e->ndpt, ncap) != 0) return -1;
+    if (arp_cap) memcpy(e->arpt.entries, arp, arp_cap * sizeof(arp_entry_t));
+    if (ndp_cap) memcpy(e->ndpt.entries, ndp, ndp_cap * sizeof(ndp_entry_t));
+    memset(&e->tx, 0, sizeof e->tx);
+    memcpy(e->tx.eth_addr, eth_addr, 6);
+    e->tx.ip4_addr = ip4_addr;
+    return 0;
+}
+
+static void env_out(env_t *e, upe_arp_entry_t *arp, size_t arp_cap, upe_ndp_entry_t *ndp,
+                    size_t ndp_cap) {
+    if (arp_cap) memcpy(arp, e->arpt.entries, arp_cap * sizeof(arp_entry_t));
+    if (ndp_cap) memcpy(ndp, e->ndpt.entries, ndp_cap * sizeof(ndp_entry_t));
+    arp_table_destroy(&e->arpt);
+    ndp_table_destroy(&e->ndpt);
+}
+
+/*
+ * Process a batch (include/upe_gpu.h "Batch layout") through the reference worker.
+ * rules: insertion order (rule_table_add assigns rule_id and sorts) unless presorted.
+ * sorted_out (optional): rt->rules after the build.
+ * arp/ndp: slot arrays, updated in place by control packets exactly as the reference does.
+ * l1, counters, rule_stats[capacity]: in/out, accumulate.
+ */
+int upe_refh_process(const upe_rule_t *rules, size_t nrules, size_t capacity, int presorted,
+                     upe_rule_t *sorted_out, upe_arp_entry_t *arp, size_t arp_cap,
+                     upe_ndp_entry_t *ndp, size_t ndp_cap, const uint8_t eth_addr[6],
+                     uint32_t ip4_addr, upe_l1_state_t *l1, uint8_t *frames, const uint64_t *desc,
+                     size_t n, uint32_t *verdict, upe_counters_t *counters,
+                     upe_rule_stat_t *rule_stats) {
+    rule_table_t rt;
+    if (build_rules(&rt, rules, nrules, capacity, presorted) != 0) return -1;
+    if (sorted_out) memcpy(sorted_out, rt.rules, rt.count * sizeof(rule_t));
+    env_t e;
+    if (env_init(&e, arp, arp_cap, ndp, ndp_cap, eth_addr, ip4_addr) != 0) return -1;
+    worker_t *w = new_worker(&rt, &e.tx, &e.arpt, &e.ndpt, l1, counters, rule_stats, capacity);
+    if (!w) return -1;
+    const upe_l1_state_t l1_start = *l1;
+    t_log_nb = t_log_nf = 0;
+    int rc = run_range(w, &l1_start, frames, desc, 0, n, verdict, counters);
+    worker_out(w, l1, counters);
+    if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
+    env_out(&e, arp, arp_cap, ndp, ndp_cap);
     worker_destroy(w);
     free(w);
-    arp_table_destroy(&arpt);
-    ndp_table_destroy(&ndpt);
     rule_table_destroy(&rt);
+    return rc;
+}
+
+/*
+ * The same with the stats thread's SIGHUP reload (src/main.c:216-282) between packets at-1 and
+ * at: packets [0, at) run with table A (rules_a, capacity cap_a), then — between two bursts, as
+ * the stats thread's plain pointer stores land between the worker's bursts — w->rt becomes table
+ * B (rules_b in insertion order, rule_table_init(cap_b) + rule_table_add) and w->rule_stats a
+ * fresh calloc(cap_b) array; pkts_* and the L1 caches carry on.  Outputs: sorted_b (table B as
+ * built), stats_a[cap_a] (the old array as it was at the swap), stats_b[cap_b], and as
+ * upe_refh_process the rest.  Verdict rule indexes refer to the table each packet ran with.
+ */
+int upe_refh_process_reload(const upe_rule_t *rules_a, size_t n_a, size_t cap_a,
+                            const upe_rule_t *rules_b, size_t n_b, size_t cap_b,
+                            upe_rule_t *sorted_b, size_t at, upe_arp_entry_t *arp, size_t arp_cap,
+                            upe_ndp_entry_t *ndp, size_t ndp_cap, const uint8_t eth_addr[6],
+                            uint32_t ip4_addr, upe_l1_state_t *l1, uint8_t *frames,
+                            const uint64_t *desc, size_t n, uint32_t *verdict,
+                            upe_counters_t *counters, upe_rule_stat_t *stats_a,
+                            upe_rule_stat_t *stats_b) {
+    if (at > n) return -1;
+    rule_table_t *rt_a = malloc(sizeof *rt_a), *rt_b = malloc(sizeof *rt_b);
+    if (!rt_a || !rt_b || build_rules(rt_a, rules_a, n_a, cap_a, 0) != 0 ||
+        build_rules(rt_b, rules_b, n_b, cap_b, 0) != 0)
+        return -1;
+    if (sorted_b) memcpy(sorted_b, rt_b->rules, rt_b->count * sizeof(rule_t));
+    env_t e;
+    if (env_init(&e, arp, arp_cap, ndp, ndp_cap, eth_addr, ip4_addr) != 0) return -1;
+    worker_t *w = new_worker(rt_a, &e.tx, &e.arpt, &e.ndpt, l1, counters, NULL, cap_a);
+    if (!w) return -1;
+    const upe_l1_state_t l1_start = *l1;
+    t_log_nb = t_log_nf = 0;
+    int rc = run_range(w, &l1_start, frames, desc, 0, at, verdict, counters);
+    /* the stats thread's swap (src/main.c:237-265) */
+    rule_stat_t *new_stats = calloc(rt_b->capacity, sizeof(rule_stat_t));
+    if (!new_stats) return -1;
+    rule_stat_t *old_stats = w->rule_stats;
+    w->rule_stats = new_stats;
+    w->rt = rt_b;
+    memcpy(stats_a, old_stats, cap_a * sizeof(rule_stat_t));
+    free(old_stats); /* after the grace period, src/main.c:270-275 */
+    rule_table_destroy(rt_a);
+    free(rt_a);
+    if (rc == 0) rc = run_range(w, &l1_start, frames, desc, at, n, verdict, counters);
+    worker_out(w, l1, counters);
+    memcpy(stats_b, w->rule_stats, cap_b * sizeof(rule_stat_t));
+    env_out(&e, arp, arp_cap, ndp, ndp_cap);
+    worker_destroy(w);
+    free(w);
+    rule_table_destroy(rt_b);
+    free(rt_b);
     return rc;
 }
 

@@ -61,7 +61,6 @@ int main(void) {
   S(upe_counters_t); S(upe_batch_info_t); P(upe_batch_info_t, n_ctrl); P(upe_batch_info_t, first_ctrl);
   S(upe_rule_stat_t);
   S(upe_launch_info_t); P(upe_launch_info_t, deferred); P(upe_launch_info_t, launches);
-  P(upe_launch_info_t, overlapped);
   S(upe_gpu_batch_t); P(upe_gpu_batch_t, verdict); P(upe_gpu_batch_t, n);
   return 0;
 }
@@ -100,7 +99,6 @@ def test_struct_layouts_match_numpy_mirrors():
     assert got["upe_launch_info_t"] == LI.itemsize
     assert got["upe_launch_info_t.deferred"] == LI.fields["deferred"][1]
     assert got["upe_launch_info_t.launches"] == LI.fields["launches"][1]
-    assert got["upe_launch_info_t.overlapped"] == LI.fields["overlapped"][1]
     import ctypes
 
     from upe_amd.gpu import QueueBatch

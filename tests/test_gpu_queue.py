@@ -1,11 +1,10 @@
-"""GPU: the overlapped worker loop (upe_gpu_process_queue_emit) — consecutive launches on two
-streams, each dispatched once its predecessor's workgroups are all resident and waiting inside
-the kernel for its predecessor's finished-workgroup count — gives exactly what the same batches
-give as one upe_gpu_process_emit() call after another: every verdict word (UPE_VF_L1_INIT
-included: both are per batch), record, counter, rule_stat and the final L1 state, on ragged
-batches, look-back-live batches and under a second context's concurrent queue.  The worker
-state carried from batch to batch is the reference's (src/worker.c:255-307 over
-src/worker.c:186-195, 218-225)."""
+"""GPU: the worker loop queued from native code (upe_gpu_process_queue_emit, one launch per
+batch) gives exactly what the same batches give as one upe_gpu_process_emit() call after
+another: every verdict word (UPE_VF_L1_INIT included: both are per batch), record, counter,
+rule_stat and the final L1 state, on ragged batches (an empty one among them), look-back-live
+batches and beside a second context's concurrent queue; a batch without records is refused
+before anything is queued.  The worker state carried from batch to batch is the reference's
+(src/worker.c:255-307 over src/worker.c:186-195, 218-225)."""
 from __future__ import annotations
 
 import threading
@@ -19,12 +18,6 @@ from upe_amd import gpu, synth
 from upe_amd.layout import desc_offsets
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.fixture(autouse=True)
-def _overlap_on(monkeypatch):
-    """The overlap is opt-in (read when a context first queues): these tests exercise it."""
-    monkeypatch.setenv("UPE_GPU_OVERLAP", "1")
 
 
 def _run(w, wl, bounds, queue: bool):
@@ -51,12 +44,12 @@ def _both(factory, wl, bounds):
         w = factory(wl.capacity)
         try:
             w.configure(wl)
-            before = w.launch_info()["overlapped"]
+            before = w.launch_info()["launches"]
             frames, verdict, rec = _run(w, wl, bounds, queue)
             counters, stats = w.get_stats()
             out.append(dict(frames=frames, verdict=verdict, rec=rec, counters=counters,
                             stats=stats, l1=w.get_l1(),
-                            overlapped=w.launch_info()["overlapped"] - before))
+                            launches=w.launch_info()["launches"] - before))
         finally:
             w.close()
     return out
@@ -85,7 +78,7 @@ def _against_oracle(q, wl, what):
 
 @pytest.mark.parametrize("config,n,cuts", [
     ("B", 600_000, [262_144, 262_209, 400_000, 400_001]),
-    ("C", 500_000, [1, 64, 100_000, 300_000, 300_063]),
+    ("C", 500_000, [1, 64, 100_000, 100_000, 300_000, 300_063]),   # an empty batch in the middle
     ("B", 40_000, list(range(1000, 40_000, 1000))),
     ("C", 48_000, list(range(3000, 48_000, 3000))),
 ])
@@ -96,8 +89,7 @@ def test_queue_equals_sequential(gpu_worker_factory, config, n, cuts):
     q, s = _both(gpu_worker_factory, wl, bounds)
     what = f"queue {config} {n} in {len(bounds) - 1}"
     _check(q, s, wl, what)
-    assert q["overlapped"] == len(bounds) - 2, q["overlapped"]
-    assert s["overlapped"] == 0
+    assert q["launches"] == s["launches"], (q["launches"], s["launches"])
     _against_oracle(q, wl, what)
 
 
@@ -125,7 +117,6 @@ def test_queue_lookback_live(gpu_worker_factory, first_hit):
     bounds = [0, 100_000, 150_000, 150_002, 220_000, n]
     q, s = _both(gpu_worker_factory, wl, bounds)
     _check(q, s, wl, f"look-back queue first_hit={first_hit}")
-    assert q["overlapped"] == len(bounds) - 2
     _against_oracle(q, wl, f"look-back queue first_hit={first_hit}")
 
 
@@ -201,11 +192,28 @@ def test_queue_two_contexts_concurrently(gpu_worker_factory):
         _against_oracle(q, wls[i], f"concurrent queue {i}")
 
 
-def test_queue_large_tables_fall_back(gpu_worker_factory):
-    """Tables over 4096 rules (rule_stats by a group-by launch after each classify): the queue
-    runs its batches one after another, with the same results."""
+def test_queue_large_tables(gpu_worker_factory):
+    """Tables over 4096 rules (rule_stats by a group-by launch after each classify)."""
     wl = synth.config_d(n=40_000)
     bounds = [0, 10_000, 10_001, 25_000, 40_000]
     q, s = _both(gpu_worker_factory, wl, bounds)
     _check(q, s, wl, "queue D")
-    assert q["overlapped"] == 0
+    _against_oracle(q, wl, "queue D")
+
+
+def test_queue_rejects_missing_records(gpu_worker_factory):
+    """A batch of n > 0 packets without records: the call fails and queues nothing."""
+    wl = synth.config_b(n=4096, seed=3)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        b = gpu.DeviceBatch(w, wl.frames, wl.desc)
+        b.hdr = w.malloc(16 * wl.n)
+        before = w.launch_info()["launches"]
+        with pytest.raises(gpu.UpeGpuError):
+            w.process_queue_emit([(b.frames, b.desc, b.verdict, b.hdr, 2048),
+                                  (b.frames, b.desc, b.verdict, 0, 2048)])
+        assert w.launch_info()["launches"] == before
+        b.free()
+    finally:
+        w.close()

@@ -53,7 +53,7 @@ def test_ring_equals_one_stream(gpu_worker_factory, config, per, count):
                  {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                   "rule_stats": r.rule_stats, "l1": r.l1}, f"ring {config} {per}x{count}")
     if per >= 262144:   # at least one tile of every batch per persistent workgroup: stamped
-        assert info["variant"] & 16, info
+        assert info["variant"] & gpu.VAR_RING, info
         assert np.all(stamps > 0), stamps
         assert stamps[-1] >= stamps[0]
     else:

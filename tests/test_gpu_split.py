@@ -17,7 +17,7 @@ from upe_amd import gpu, synth
 
 pytestmark = pytest.mark.gpu
 
-VAR_SPLIT = 128
+VAR_SPLIT = gpu.VAR_SPLIT
 
 
 def _split_run(w, wl):

@@ -261,3 +261,36 @@ def test_restated_flow_hash_matches_reference(case):
         assert (rc == 0) == bool(parsed[i]), i
         got = lib.upe_ref_flow_hash(_p(key)) if rc == 0 else 0
         assert got == int(want[i]), i
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference harness not built here")
+@pytest.mark.parametrize("name", ["B", "C"])
+def test_reference_reload_hook_equals_two_segments(name):
+    """oracle/ref_harness.c's SIGHUP-reload hook (one reference worker_t, w->rt and w->rule_stats
+    swapped between two bursts as src/main.c:258-265 does) equals the restated worker run in two
+    segments: table A up to the reload point, then table B with a fresh rule_stats and the
+    counters, L1 caches and neighbour tables carried over."""
+    import dataclasses
+
+    import reload_util
+    from upe_amd.layout import RULE_STAT_DTYPE
+
+    wl, rules_b, at, cap_b = reload_util.case(name)
+    r, old = oracle.run_reference_reload(wl, rules_b, cap_b, at)
+    assert np.array_equal(r.rules_sorted, synth.build_rule_table(rules_b))
+    wa = dataclasses.replace(wl, desc=wl.desc[:at])
+    ra = oracle.run_restated(wa)
+    wb = dataclasses.replace(wl, frames=ra.frames, desc=wl.desc[at:], arp=ra.arp, ndp=ra.ndp,
+                             capacity=cap_b)
+    rb = oracle.run_restated(wb, rules_sorted=r.rules_sorted, l1=ra.l1, counters=ra.counters,
+                             rule_stats=np.zeros(cap_b, RULE_STAT_DTYPE))
+    assert np.array_equal(old, ra.rule_stats)
+    assert np.array_equal(r.rule_stats, rb.rule_stats)
+    assert np.array_equal(r.verdict[:at] & ~np.uint32(0x80), ra.verdict & ~np.uint32(0x80))
+    assert np.array_equal(r.verdict[at:] & ~np.uint32(0x80), rb.verdict & ~np.uint32(0x80))
+    assert np.array_equal(r.frames, rb.frames)
+    assert r.counters.tobytes() == rb.counters.tobytes()
+    assert r.l1.tobytes() == rb.l1.tobytes()
+    # the reload changed what happens to some packets (the test is not vacuous)
+    plain = oracle.run_reference(wl)
+    assert not np.array_equal(plain.verdict, r.verdict)

@@ -122,46 +122,19 @@ constexpr uint32_t kNdpLdsSlots = UPE_NDP_LDS_SLOTS;
 constexpr size_t kLdsDynMax = 136 * 1024;
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
+constexpr int kRingMax = 64;           // batches of a ring launch whose completion is stamped
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
 // 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 256 no fold of the
 // previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
-// Header windows in two steps (bytes 48..79 only for frames that need them): 0 off, 1 the rest
-// requested when the window is consumed, 2 at the end of the chunk before (diagnostic builds)
-#ifndef UPE_WIN48
-#define UPE_WIN48 0
-#endif
-constexpr int kWin48 = UPE_WIN48;
-// Cache-policy bits of the emit-mode record store (buffer aux: 1 sc0, 2 nt, 16 sc1; 0 = a plain
-// store).  sc1 writes the records through and drops their lines from the XCD's L2, so the end
-// of a launch has ~16 MB less dirty data to write back at the kernel boundary: config B
-// 24.5 -> 24.1 us per 1M batch (nt 24.5, sc0 sc1 24.2, nt sc1 24.2).
-#ifndef UPE_REC_AUX
-#define UPE_REC_AUX 16
-#endif
-constexpr int kRecAux = UPE_REC_AUX;
-// The verdict words written through too (one dword per lane, coalesced): B 24.25 -> 24.1 us.
-// In-place header stores written through (UPE_FRAME_SC1) were slower: 33.7 -> 35.4 us.
-#ifndef UPE_VERDICT_SC1
-#define UPE_VERDICT_SC1 1
-#endif
-constexpr bool kVerdictSc1 = UPE_VERDICT_SC1;
-#ifndef UPE_FRAME_SC1
-#define UPE_FRAME_SC1 0
-#endif
-#ifndef UPE_DIAG_NO_DONE
-#define UPE_DIAG_NO_DONE 0   // diagnostic timing builds only: no deferred-candidate repair
-#endif
-// Overlapped queue launches: s_sleep argument (units of 64 clocks) between wave 0's polls of the
-// previous launch's finished-workgroup count.
-#ifndef UPE_DIAG_Q_NOWAIT
-#define UPE_DIAG_Q_NOWAIT 0   // diagnostic timing builds only: queue launches do not wait
-#endif
-#ifndef UPE_Q_POLL_SLEEP
-#define UPE_Q_POLL_SLEEP 4
-#endif
+// Cache policy of the emit-mode record store: sc1 (buffer aux 16) writes the records through
+// and drops their lines from the XCD's L2, so the end of a launch has ~16 MB less dirty data to
+// write back at the kernel boundary (config B 24.5 -> 24.1 us per 1M batch; nt 24.5, sc0 sc1
+// 24.2).  The verdict words are written through too (B 24.25 -> 24.1 us); the in-place 16-byte
+// header stores are not (written through they were slower: 33.7 -> 35.4 us, partial lines).
+constexpr int kRecAux = 16;
 
 // ---- compiled rule table (built by upe_gpu_load_rules) --------------------------------------
 // rv4[i]: header + first address word, used for every packet:
@@ -221,8 +194,7 @@ struct __attribute__((aligned(128))) BatchAcc {
     uint32_t pad0[30];
     // look-back give-ups (a launch that started from a disagreeing L1 entry): workgroups that have
     // finished, deferred (chunk, family) entries, and "some wave gave up" (later waves then wait
-    // for no unpublished flag at all).  A line of their own: the batch's launch polls them
-    // while an overlapped next launch may read grid and n.
+    // only briefly for an unpublished flag).  A line of their own: the launch polls them.
     uint32_t done, ndefer, giveup;
     uint32_t pad[29];
 };
@@ -242,9 +214,7 @@ enum { LB_FP4 = 1, LB_FP6 = 2, LB_KNOWN4 = 4, LB_INCL4 = 8, LB_KNOWN6 = 16, LB_I
 constexpr uint32_t kLbTagMod = 0x3FFFFFFu;   // tags 1 .. kLbTagMod
 
 // Everything a batch reads or writes besides the packets and the tables, in one device
-// allocation.
-// One L1 state slot per 128-byte line: overlapped launches (upe_gpu_process_queue_emit) read one
-// slot while the other is written, and a line another XCD's L2 holds must not carry both.
+// allocation.  One L1 state slot per 128-byte line.
 struct __attribute__((aligned(128))) L1Slot {
     DevL1 s;
 };
@@ -252,12 +222,6 @@ struct DevState {
     L1Slot l1[2];
     BatchAcc acc[3];
     unsigned long long totals[8];                           // cumulative, upe_counters_t order
-    // overlapped launches (upe_gpu_process_queue_emit): workgroups of counting launches finished
-    // and started (cumulative; Args::fin_flags)
-    uint32_t fin;
-    uint32_t pad0[31];
-    uint32_t started;
-    uint32_t pad1[31];
     unsigned long long acc_stats[kReps][2 * kSmallRules];   // small tables, per sorted index
     uint32_t census[32];                                     // residency census (census_probe)
     TilePay* pay;                    // [grid]
@@ -290,36 +254,22 @@ struct NeighIndex {
 struct __attribute__((aligned(16))) TssGroup {
     uint32_t w[16];
 };
-// An IPv4 slot is one uint4 (UPE_TSS_SLOT16, the default): the masked key's free bits carry the
-// rest — k0's low byte (the IP version, never part of a group's mask) and k1's high half (above
-// the 16-bit destination port) hold v = (index + 1) | action << 22 (0 = empty slot), so a probe
-// is one 16-byte load, one memory request (two loads into one line were two requests:
-// tools/fetch_calib), and the IPv4 slot array takes half the L2.
-#ifndef UPE_TSS_SLOT16
-#define UPE_TSS_SLOT16 1
-#endif
-constexpr bool kTssSlot16 = UPE_TSS_SLOT16;
-constexpr int kTssSlot4 = kTssSlot16 ? 1 : 2, kTssSlot6 = 3;   // uint4 per slot
+// An IPv4 slot is one uint4: the masked key's free bits carry the rest — k0's low byte (the IP
+// version, never part of a group's mask) and k1's high half (above the 16-bit destination port)
+// hold v = (index + 1) | action << 22 (0 = empty slot), so a probe is one 16-byte load, one
+// memory request (two loads into one line were two requests: tools/fetch_calib), and the IPv4
+// slot array takes half the L2 (config D 755 -> 716 us per 16M against 32-byte slots).
+constexpr int kTssSlot4 = 1, kTssSlot6 = 3;   // uint4 per slot
 constexpr uint32_t kTssMaxRules = 1u << 22;   // index + 1 in 22 bits, the action above it
 // Fingerprints of small groups staged in LDS (word [15] of such a group: 1 + its offset in the
 // staged image): their probes then wait for no fingerprint round trip.
-#ifndef UPE_FP_STAGE_MAX
-#define UPE_FP_STAGE_MAX 8192
-#endif
-constexpr uint32_t kFpStageMax = UPE_FP_STAGE_MAX;    // staged fingerprints (2 bytes each)
-constexpr uint32_t kFpStageGroup = 4096;             // largest group (slots) staged
+constexpr uint32_t kFpStageMax = 8192;     // staged fingerprints (2 bytes each)
+constexpr uint32_t kFpStageGroup = 4096;   // largest group (slots) staged
 // Groups whose fingerprints are not staged are probed without them: slot t1 (where cuckoo
 // placement leaves ~80 % of the keys at this load), then t2 if t1 holds another key.  One round
 // trip for most hits instead of a fingerprint trip followed by a slot trip (config D 808 -> 775
 // us); a miss takes two slot reads.
-#ifndef UPE_TSS_DIRECT
-#define UPE_TSS_DIRECT 1
-#endif
-constexpr bool kTssDirect = UPE_TSS_DIRECT;
-#ifndef UPE_TSS_RATIO_X2
-#define UPE_TSS_RATIO_X2 5
-#endif
-constexpr uint32_t kTssRatioX2 = UPE_TSS_RATIO_X2;   // tuple-space slots >= ratio / 2 x keys
+constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 
 struct Args {
     uint8_t* frames;
@@ -338,8 +288,6 @@ struct Args {
     const TssGroup* tg6;
     const uint4* tt4;
     const uint4* tt6;
-    const uint16_t* tf4;           // per slot: 16-bit fingerprint of its key, 0 = empty
-    const uint16_t* tf6;
     const uint4* tfs;              // staged fingerprint image (Args::fp_lds uint4 go to LDS)
     uint32_t ng4, ng6, tss;
     // the context's arrays, passed by value so that no kernel waits on a pointer load
@@ -372,15 +320,6 @@ struct Args {
     uint32_t* ring_wg;
     unsigned long long* ring_done;
     unsigned long long* ring_t0;
-    // overlapped launches (upe_gpu_process_queue_emit): bit 0 this launch counts its finished
-    // workgroups into st->fin once every wave's stores have drained; bit 1 its workgroups wait,
-    // after the table staging, until st->fin reaches fin_wait (the previous launch, on another
-    // stream, has finished); bit 2 its workgroups count themselves started into st->started,
-    // and the one that brings it to start_target stores launch_tag into the signal word `sig`
-    // (the next launch's stream waits for that before it dispatches: every workgroup of this
-    // launch is resident before any of the next, so the next one's wait always ends)
-    uint32_t fin_flags, fin_wait, start_target;
-    unsigned long long* sig;
     // header-split batch (upe_gpu_process_split_emit): bytes 0..63 of packet i at slab[4 i ..
     // 4 i + 3] (zero past len); bytes 64.. from the frame.  nullptr: every byte from the frame.
     const uint4* slab;
@@ -476,44 +415,9 @@ __device__ __forceinline__ uint32_t csum_fold(unsigned long long sum) {
     return (~f) & 0xFFFFu;
 }
 __device__ __forceinline__ void store16(uint4* p, uint4 v) { *p = v; }
-// Frame-window and descriptor loads (diagnostic UPE_LOAD_NT: bit 0 frames, bit 1 descriptors as
-// non-temporal loads: read once, streamed).
-#ifndef UPE_LOAD_NT
-#define UPE_LOAD_NT 0
-#endif
-// The host paths' launches (upe_gpu_process_mapped over host memory, ~1.3-1.5 ms per 1M packets,
-// link-bound; upe_gpu_process_host's chunks in device slots) run their own kernel instantiations
-// (variant bit 6), so that a profile keeps them apart from the device-resident launches of the
-// same configuration.  UPE_HOST_NT=1 makes their frame and descriptor loads
-// streaming (non-temporal) loads: measured slower (config B mapped 537 vs 666-680 Mpps in place,
-// C 214 vs 319; profiles/r03/v5_host_nt_ab.txt), so off.
-#ifndef UPE_HOST_NT
-#define UPE_HOST_NT 0
-#endif
-template <bool kHostMem = false>
-__device__ __forceinline__ uint4 ldf(const uint4* p) {
-    if ((UPE_LOAD_NT & 1) || (kHostMem && UPE_HOST_NT)) {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-        return make_uint4(x[0], x[1], x[2], x[3]);
-    }
-    return *p;
-}
-template <bool kHostMem = false>
-__device__ __forceinline__ uint64_t ldd(const uint64_t* p) {
-    if ((UPE_LOAD_NT & 2) || (kHostMem && UPE_HOST_NT)) return __builtin_nontemporal_load(p);
-    return *p;
-}
-// The in-place header stores (diagnostic UPE_FRAME_SC1: written through, lines dropped from L2).
-__device__ __forceinline__ void store16_frame(uint4* p, uint4 v) {
-#if UPE_FRAME_SC1
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
-#else
-    *p = v;
-#endif
-}
+// Frame windows and descriptors are plain (cached) loads: non-temporal ones measured slower for
+// device batches (C +12 us, B +6.5 us per 1M) and for host-memory batches (config B mapped 537
+// vs 666-680 Mpps in place, C 214 vs 319; profiles/r03/v5_host_nt_ab.txt).
 
 // ---- neighbour lookups ----------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t fold_v6(const uint32_t ip[4]) {
@@ -712,16 +616,9 @@ __global__ void upe_l1_sync(DevL1* l1, BatchAcc* acc, const TilePay* pay) {
 // without IPv6 address words skip the rv6 test (a scalar branch).
 // Small tables are read from an LDS copy (staged at kernel entry, broadcast reads of a
 // wave-uniform address: no scalar-cache round trip in the dependent chain); larger ones through
-// the scalar unit from the constant address space.
-// UPE_RULE_PREFIX=1 (measured, off): larger tables get their first kSmallRules rules staged in
-// LDS too, scanned from there before the rest goes through the scalar unit, so a wave whose
-// packets all match early (config C: every wave within its first 12 rules) waits on no scalar
-// load.  Parity-green, but B 43.5-43.6 vs 43.8-44.1 Gpps and C 39.55 vs 39.3 us per batch
-// (profiles/r03/v8_rule_prefix_ab.txt): C's rule words already hit in the scalar cache.
-#ifndef UPE_RULE_PREFIX
-#define UPE_RULE_PREFIX 0
-#endif
-constexpr bool kRulePrefix = UPE_RULE_PREFIX;
+// the scalar unit from the constant address space.  (Staging the first 64 rules of larger
+// tables in LDS too measured slower, profiles/r03/v8_rule_prefix_ab.txt: C's rule words already
+// hit in the scalar cache.)
 template <bool V6, bool kLdsRules>
 __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4],
@@ -807,7 +704,6 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
     const uint32_t ngf = is6 ? a.ng6 : a.ng4;
     const auto* G4 = as_const<u32x16>(a.tg4);
     const auto* G6 = as_const<u32x16>(a.tg6);
-    const uint16_t* FP = is6 ? a.tf6 : a.tf4;
     const uint4* T = is6 ? a.tt6 : a.tt4;
     const uint32_t st = is6 ? (uint32_t)kTssSlot6 : (uint32_t)kTssSlot4;   // slot stride in uint4
     for (uint32_t g = 0; g < ng; ++g) {
@@ -854,26 +750,23 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
             const uint32_t t1 = q[13] + slot1(h, q[12], q[11]);
             const uint32_t t2 = q[13] + slot2(h, q[12], q[11]);
             const uint32_t tag = tss_tag(h);
-            // fingerprints from LDS when the group's are staged, else from memory
+            // fingerprints from LDS when the group's are staged; otherwise none: slot t1, then t2
             const uint32_t so = sfp ? (is6 ? q6[15] : q4[15]) : 0u;
-            uint32_t f1, f2;
+            uint32_t f1 = tag, f2 = tag;
             if (so) {
                 const uint32_t b = so - 1u - q[13];
                 f1 = sfp[b + t1];
                 f2 = sfp[b + t2];
-            } else if (kTssDirect) {
-                f1 = f2 = tag;   // no fingerprints: slot t1, then t2
-            } else {
-                f1 = FP[t1];
-                f2 = FP[t2];
             }
             const bool m1 = f1 == tag, m2 = f2 == tag;
             uint32_t idx = kNone, ac = 0;
             auto probe = [&](uint32_t t) {
                 const uint4 A = T[st * t];
                 uint4 B = make_uint4(0, 0, 0, 0), C = B;
-                if (is6 || !kTssSlot16) B = T[st * t + 1];
-                if (is6) C = T[st * t + 2];
+                if (is6) {
+                    B = T[st * t + 1];
+                    C = T[st * t + 2];
+                }
                 const bool k4 = A.x == kw[0] && A.y == kw[1] && A.z == kw[2] && A.w == kw[3];
                 // the compact IPv4 slot: v = (index + 1) | action << 22 in the key's free bits
                 const uint32_t v = (A.x & 0xFFu) | ((A.y >> 16) << 8);
@@ -882,10 +775,10 @@ __device__ __forceinline__ uint32_t tss_match_both(const Args& a, bool active, b
                 const bool hit = is6 ? ((C.w & 1u) && k4 && B.x == kw[4] && B.y == kw[5] &&
                                         B.z == kw[6] && B.w == kw[7] && C.x == kw[8] &&
                                         C.y == kw[9])
-                                     : kTssSlot16 ? (v != 0u && k4c) : (B.y != 0u && k4);
+                                     : (v != 0u && k4c);
                 if (hit) {
-                    idx = is6 ? C.z : kTssSlot16 ? (v & (kTssMaxRules - 1u)) - 1u : B.x;
-                    ac = is6 ? (C.w >> 8) : kTssSlot16 ? v >> 22 : B.z;
+                    idx = is6 ? C.z : (v & (kTssMaxRules - 1u)) - 1u;
+                    ac = is6 ? (C.w >> 8) : v >> 22;
                 }
                 return hit;
             };
@@ -1113,10 +1006,7 @@ __device__ uint32_t lookback(const uint32_t* lb, uint32_t chunk, uint32_t tag, u
 // F6 = the first chunk holding a miss-then-hit packet of each family; a deferred candidate of
 // chunk c takes the starting entry's MAC iff F >= c (the earlier lanes of its own chunk were
 // checked when it deferred).  entries[e] = packet index | family << 31 (1 = IPv6).
-#ifndef UPE_REPAIR_UNROLL
-#define UPE_REPAIR_UNROLL 4
-#endif
-constexpr int kRepairUnroll = UPE_REPAIR_UNROLL;
+constexpr int kRepairUnroll = 4;
 struct Repair {
     uint32_t mac4_lo, mac4_hi, mac6_lo, mac6_hi;   // the batch's starting L1 entries' MACs
 };
@@ -1221,7 +1111,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kQueue = false, bool kHost = false, bool kSplit = false>
+          bool kHost = false, bool kSplit = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1231,9 +1121,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
     __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
-    __shared__ uint32_t s_bdone[kRing ? 4 : 1];   // ring: chunks finished per batch (4 in flight)
-    __shared__ uint32_t s_fin;     // queue launches: waves finished (fin_flags bit 0)
-    __shared__ uint32_t s_qready;  // queue launches: wave 0 has seen the previous launch finish
+    __shared__ uint32_t s_bdone[kRing ? kRingMax : 1];   // ring: the workgroup's chunks done per batch
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -1266,7 +1154,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
                 if (c < 3 || len > 16u * c) {
-                    const uint4 v = ldf<kHost>(c < 4 ? &h[c] : &q[c]);
+                    const uint4 v = c < 4 ? h[c] : q[c];
                     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
                 }
             }
@@ -1286,25 +1174,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
             const uint4* h = kSplit ? a.slab + 4 * (size_t)pi : q;
-            v.c0 = ldf<kHost>(&h[0]); v.c1 = ldf<kHost>(&h[1]); v.c2 = ldf<kHost>(&h[2]);
-            if (!kWin48) {
-                if (len > 48u) v.c3 = ldf<kHost>(&h[3]);
-                if (len > 64u) v.c4 = ldf<kHost>(&q[4]);
-            }
+            v.c0 = h[0]; v.c1 = h[1]; v.c2 = h[2];
+            if (len > 48u) v.c3 = h[3];
+            if (len > 64u) v.c4 = q[4];
         }
         return v;
-    };
-    // kWin48: bytes 48..79 only for the frames that use them.  An option-less IPv4 frame (byte 14
-    // 0x45) needs bytes 0..46 on every path (the TCP data offset is byte 46); IPv6, IPv4 with
-    // options, ARP and the rest take bytes 48..79 once bytes 12..14 have arrived.
-    auto fetch_rest = [&](uint64_t dsc, bool live, uint4 c0, uint4& c3, uint4& c4) {
-        const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
-        const bool opt4 = (c0.w & 0xFFFFFFu) == 0x450008u;   // bytes 12..14: 08 00 45
-        if (live && len > 48u && !opt4) {
-            const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            c3 = q[3];
-            if (len > 64u) c4 = q[4];
-        }
     };
     Win nw;
     bool have_nw = false;   // nw holds the window of the wave's next chunk
@@ -1321,9 +1195,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         return t < a.ntiles && c * 64u < a.n ? c : kNone;
     };
     if (tid == 0) s_claim = kWaves;
-    if (kQueue && tid == 0) s_fin = 0u;
-    if (kQueue && tid == 0) s_qready = 0u;
-    if (kRing && tid < 4) s_bdone[tid] = 0u;
+    if (kRing)
+        for (uint32_t k = tid; k < (uint32_t)kRingMax; k += kBlock) s_bdone[k] = 0u;
     if (kRing && tid == 0)   // the ring's time origin: the first workgroup to start
         __hip_atomic_fetch_min(a.ring_t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1334,10 +1207,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // rule tables into LDS, before the entry barrier.  (Issuing the first chunk's window loads
     // here too queues the staging loads behind them: B 26.3 -> 27.6 us, C 40.1 -> 43.8 us.)
     uint64_t dsc_next = 0;
-    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[ch * 64u + lane]);
-    if (!kTssMode && (small_stats || kRulePrefix)) {
-        // the whole table (small tables) or its first kSmallRules rules (the scan's LDS prefix)
-        const uint32_t nst = a.nrules_pad < (uint32_t)kSmallRules ? a.nrules_pad : (uint32_t)kSmallRules;
+    if (ch != kNone && ch * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[ch * 64u + lane];
+    if (!kTssMode && small_stats) {
+        // small tables: the whole table
+        const uint32_t nst = a.nrules_pad;
         const uint4* g4 = reinterpret_cast<const uint4*>(a.rv4);
         const uint4* g6 = reinterpret_cast<const uint4*>(a.rv6);
         uint4* d4 = reinterpret_cast<uint4*>(s_rv4);
@@ -1349,19 +1222,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // outcome folded in (its replicated minima / maxima, then at most two payload loads).
     // DevL1 words: arp_ip, arp_mac_lo/hi, ndp_ip[4], ndp_mac_lo/hi, arp_ok, ndp_ok.
     static_assert(sizeof(DevL1) == 64, "DevL1 is one scalar load");
-    // (A queue launch loads them once the previous launch has finished: below.)
-    u32x16 lin;
+    const u32x16 lin = *as_const<u32x16>(l1_in(a));
     unsigned long long pr[R_N] = {0, 0, 0, 0};
-    const bool q_wait = kQueue && (a.fin_flags & 2u);   // a queue launch after the first
-    auto load_prev = [&]() {
-        lin = *as_const<u32x16>(l1_in(a));
-        if (lane < kReps)
-            for (int j = 0; j < R_N; ++j)
-                pr[j] = kQueue ? __hip_atomic_load(&acc_prev(a)->l1r[lane][j], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : acc_prev(a)->l1r[lane][j];
-    };
-    if (!kQueue) load_prev();
+    if (lane < kReps)
+        for (int j = 0; j < R_N; ++j) pr[j] = acc_prev(a)->l1r[lane][j];
     // small neighbour indexes into LDS after the rule-stats bins: a lookup is then an LDS read,
     // not a memory round trip queued behind the batch's frame traffic
     uint4* s_arp = reinterpret_cast<uint4*>(lds_hist + (lds_stats ? 2 * a.nrules_pad : 0u));
@@ -1402,7 +1266,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (blockIdx.x == 0) {
             // workgroup 0: this batch's grid and size, batch k + 1's accumulators re-armed
             // (batch k - 2's, folded by batch k - 1)
-            // (written through: an overlapped next launch reads them from another XCD)
             if (lane == 0) {
                 st_wt(&acc_cur(a)->grid, gridDim.x);
                 st_wt(&acc_cur(a)->n, a.n);
@@ -1416,33 +1279,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
     };
     auto fold_start = [&]() {
-        if (q_wait) {
-            // The previous launch runs on another stream and may not have finished (this wave's
-            // first window loads are in flight meanwhile): wait for its finished-workgroup count
-            // (every workgroup of it is resident: fin_flags bit 2).  Everything this launch reads
-            // of the previous one's (L1 state, accumulators, payloads) was stored write-through
-            // or by atomics and drained before that count, on lines nothing here has touched
-            // since this launch began.
-            // One poller per workgroup (wave 0, which always reaches this point: with its first
-            // chunk or after the loop); the other waves wait for its word in LDS.  (Every wave
-            // polling the one device word put ~70 k loads per us on one memory channel while the
-            // previous launch's tail was still running through it.)
-            if (UPE_DIAG_Q_NOWAIT) {
-                // diagnostic timing builds only: no wait (results wrong)
-            } else if (wave == 0) {
-                while ((int32_t)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                     &a.st->fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
-                                 a.fin_wait) < 0)
-                    __builtin_amdgcn_s_sleep(UPE_Q_POLL_SLEEP);
-                if (lane == 0)
-                    __hip_atomic_store(&s_qready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                           &s_qready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
-                    __builtin_amdgcn_s_sleep(2);
-            }
-            load_prev();
-        }
         if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
 #pragma unroll
             for (int j = 0; j < 11; ++j) L1[j] = lin[j];
@@ -1454,17 +1290,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
         folded = true;
     };
-    // A queue launch counts its workgroups started (after the staging, so that the atomic's
-    // round trip is not in front of the staging loads): the one that completes the count stores
-    // the launch tag into the signal word the next launch's stream waits on.
-    if (kQueue && (a.fin_flags & 4u) && tid == 0) {
-        const uint32_t t = __hip_atomic_fetch_add(&a.st->started, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if (t + 1u == a.start_target)
-            __hip_atomic_store(a.sig, a.launch_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (kQueue && !q_wait) load_prev();
-    if (!q_wait && wave == 0 && blockIdx.x < 8) books();
+    if (wave == 0 && blockIdx.x < 8) books();
 
     // Persistent workgroups: the grid is what the chip holds at once, so the per-workgroup
     // flush happens once per workgroup, at the very end of its life.  (Per-wave claims from
@@ -1511,7 +1337,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         uint8_t* p = a.frames + ((size_t)off16 << 4);
         uint32_t w[20];
         if (kMid && have_nw) {
-            if (kWin48 == 1) fetch_rest(dsc, live, nw.c0, nw.c3, nw.c4);
             const uint4 c[5] = {nw.c0, nw.c1, nw.c2, nw.c3, nw.c4};
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
@@ -1522,7 +1347,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
         have_nw = false;
         dsc_next = 0;
-        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[chn * 64u + lane]);
+        if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
         if (!folded) fold_start();
 
         if (first) STAMP_VM(2);
@@ -1605,19 +1430,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else if (kTssMode) {
             ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act, s_fps);
         } else {
-            // small tables: all in LDS; larger ones: the LDS-staged first kSmallRules rules, then
-            // (only while some lane is unmatched) the rest through the scalar unit
-            const uint32_t nl = small_stats ? a.nrules_pad
-                                            : (kRulePrefix ? (uint32_t)kSmallRules : 0u);
-            ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nl)
-                         : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nl);
-            if (!small_stats && __any(ok && ri == kNone)) {
-                const bool fin = !ok || ri != kNone;   // matched lanes take no later rule
-                const uint32_t r2 =
-                    need_v6 ? scan_rules<true, false>(a, fin, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, nl, a.nrules_pad)
-                            : scan_rules<false, false>(a, fin, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, nl, a.nrules_pad);
-                if (ri == kNone) ri = r2;
-            }
+            // small tables from their LDS copy, larger ones through the scalar unit
+            const uint32_t nr = a.nrules_pad;
+            if (small_stats)
+                ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
+                             : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
+            else
+                ri = need_v6 ? scan_rules<true, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
+                             : scan_rules<false, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
         }
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
@@ -1694,9 +1514,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const uint32_t need = (__ballot(c4) ? (uint32_t)LB_FP4 : 0u) |
                                   (__ballot(c6) ? (uint32_t)LB_FP6 : 0u);
             if (need) {
-                // once any wave of the launch has given up, wait for no unpublished flag at all
+                // once any wave of the launch has given up, wait only briefly (1/16 of the bound)
+                // for an unpublished flag: the workgroup it belongs to is likely not resident,
+                // but a short wait still resolves the flags that are merely in flight, so that
+                // the give-up does not cascade into a long serial repair
                 const uint32_t spin = __hip_atomic_load(&acc_cur(a)->giveup, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT) ? 0u : a.lb_spin;
+                                                        __HIP_MEMORY_SCOPE_AGENT) ? a.lb_spin / 16u : a.lb_spin;
                 uint32_t before = 0;
                 const uint32_t left = lookback(a.lb, chunk, a.lb_tag, need, lane, spin, before);
                 const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1752,9 +1575,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
                              : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
             }
-            if (kRecAux == 0) {
-                a.hdr[i] = rec;
-            } else {   // diagnostic: the record store with cache-policy bits (UPE_REC_AUX)
+            {   // a buffer store with the write-through cache policy (kRecAux)
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.hdr, 0, 0x7FFFFFF0, 0x00020000);
                 __builtin_amdgcn_raw_buffer_store_b128(v4u{rec.x, rec.y, rec.z, rec.w}, rs, i * 16u, 0,
@@ -1763,17 +1584,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else if (live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
-                store16_frame(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
+                store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
                                                 (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
-            if (wrote1) store16_frame(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
+            if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
-        if (live) {
-            if (kVerdictSc1)   // written through (sc1): no dirty lines left for the boundary
-                __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            else
-                a.verdict[i] = code | flags | rbits;
-        }
+        if (live)   // written through (sc1): no dirty lines left for the boundary
+            __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         // 2 B/packet for upe_rule_hist (lean linear-scan launches never have the array; the
         // tuple-space tables it serves always do)
         if ((kTssMode || !kLean) && a.lens16 && live) a.lens16[i] = (uint16_t)len;
@@ -1832,17 +1649,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
         if (kRing) {
             // every workgroup owns ring_mine chunks of each batch (the host launches the ring
-            // kernel only when a batch's tiles divide evenly over the grid)
+            // kernel only when a batch's tiles divide evenly over the grid, and for at most
+            // kRingMax batches: one LDS counter per batch, however far apart the workgroup's
+            // waves are)
             const uint32_t j = ch / a.ring_cpb, mine = a.ring_mine;
             uint32_t d = 0;
-            if (lane == 0) d = atomicAdd(&s_bdone[j & 3u], 1u) + 1u;
+            if (lane == 0) d = atomicAdd(&s_bdone[j], 1u) + 1u;
             d = __builtin_amdgcn_readfirstlane(d);
             if (d == mine) {   // the workgroup is done with batch j
                 uint32_t t = 0;
-                if (lane == 0) {
-                    s_bdone[j & 3u] = 0u;
-                    t = atomicAdd(&a.ring_wg[j], 1u) + 1u;
-                }
+                if (lane == 0) t = atomicAdd(&a.ring_wg[j], 1u) + 1u;
                 t = __builtin_amdgcn_readfirstlane(t);
                 if (lane == 0 && t == gridDim.x) {
                     const unsigned long long t0 = __hip_atomic_load(a.ring_t0, __ATOMIC_RELAXED,
@@ -1853,12 +1669,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 }
             }
         }
-        if (kMid && kWin48 == 2 && have_nw)
-            fetch_rest(dsc_next, chn * 64u + (uint32_t)lane < a.n, nw.c0, nw.c3, nw.c4);
         if (late) {
             chn = claim();
             dsc_next = 0;
-            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = ldd<kHost>(&a.desc[chn * 64u + lane]);
+            if (chn != kNone && chn * 64u + (uint32_t)lane < a.n) dsc_next = a.desc[chn * 64u + lane];
             asm volatile("" : "+v"(dsc_next));   // consumed here (see before the loop)
         }
     }
@@ -1877,7 +1691,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // else it has to send, while wave 0 flushes the accumulators and the other waves the
     // mid-size rule_stats, so the round trip overlaps those.
     constexpr int kCounter = kWaves > 1 ? 1 : 0;
-    const bool counting = !kNoLB && !UPE_DIAG_NO_DONE && (look4 || look6);
+    const bool counting = !kNoLB && (look4 || look6);
     if (counting && wave == kCounter) {
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(&acc_cur(a)->done, 1u);
@@ -1905,25 +1719,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             if (v) atomicAdd(&rep[k], (unsigned long long)v);
         }
     }
-    // overlapped launches: the last wave of the workgroup to drain its stores counts it finished
-    auto count_fin = [&]() {
-        if (kQueue && (a.fin_flags & 1u)) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(&s_fin, 1u);
-            t = __builtin_amdgcn_readfirstlane(t);
-            if (t + 1u == (uint32_t)kWaves && lane == 0)
-                __hip_atomic_fetch_add(&a.st->fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    };
-    if (wave != 0) {
-        count_fin();
-        return;
-    }
+    if (wave != 0) return;
     // ---- wave 0: flush the workgroup into the replicated accumulators ----
-    // (a queue launch after the first does its between-batch bookkeeping here, once the
-    // previous launch has finished: before its own count, so before the next launch's atomics)
-    if (q_wait && blockIdx.x < 8) books();
     // Device atomics are priced per wave-instruction (~50 ns per CU, whatever the lane count),
     // so every accumulator kind goes out as ONE instruction, lane k carrying field k.  Nothing
     // waits for them: the next launch reads them (kernel boundary), the host after a
@@ -1977,7 +1774,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                a.launch_tag << 2 | (L1[9] ? 1ull : 0ull) | (L1[10] ? 2ull : 0ull),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    count_fin();
     STAMP(5);
 }
 
@@ -2318,8 +2114,6 @@ struct upe_gpu_ctx {
     TssGroup* tg6 = nullptr;
     uint4* tt4 = nullptr;
     uint4* tt6 = nullptr;
-    uint16_t* tf4 = nullptr;
-    uint16_t* tf6 = nullptr;
     uint16_t* tfs = nullptr;          // staged fingerprint image
     uint32_t nfs = 0;                 // its length in uint4
     uint32_t ng4 = 0, ng6 = 0;
@@ -2357,18 +2151,6 @@ struct upe_gpu_ctx {
     uint32_t last_grid = 0;
     unsigned long long* ring_wg = nullptr;   // ring launches: per-batch counters + time origin
     size_t ring_alloc = 0;
-    // overlapped launches (upe_gpu_process_queue_emit): the finished / started workgroup counts
-    // st->fin / st->started will have reached once the launches queued so far have run, the
-    // flags and wait of the next launch, the queue's second stream, the signal word the next
-    // launch's stream waits on, and the stream of the queue's previous launch (while one runs)
-    uint32_t fin_total = 0, start_total = 0;
-    uint32_t fin_next_flags = 0, fin_next_wait = 0;
-    hipStream_t q_stream = nullptr;
-    hipEvent_t q_ev = nullptr;
-    unsigned long long* sig = nullptr;
-    hipStream_t q_prev = nullptr;
-    int overlap = -1;              // UPE_GPU_OVERLAP (default 0) and device support; -1 unknown
-    uint32_t overlapped = 0;       // launches that waited for their predecessor (launch_info)
     // every launch and state upload is ordered after the previous one, whatever its stream
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
@@ -2403,7 +2185,6 @@ struct upe_gpu_ctx {
     // host threads applying emit-mode records to the caller's frames (upe_gpu_process_host_emit)
     std::unique_ptr<struct ApplyPool> pool;
     uint32_t host_slots = 4;       // device slots of the host round trip (UPE_GPU_HOST_SLOTS, 2..8)
-    int host_serial = -1;          // UPE_GPU_HOST_SERIAL: copies back on the copy-in stream (-1: per mode)
     // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
     // device into host-mapped memory, and the first launch whose report counts
     unsigned long long* agree_h = nullptr;
@@ -2563,24 +2344,25 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 256;
+constexpr int kVarCount = 128;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
-// bit 4 ring (lean emit linear scan only), bit 5 queue (overlapped launches; emit only), bit 6
-// a host path's launch (upe_gpu_process_mapped / upe_gpu_process_host; not ring or queue), bit 7
-// a header-split batch (upe_gpu_process_split_emit; emit only, not ring, queue or host).
-int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool queue = false,
-                 bool host = false, bool split = false) {
-    return (split && emit && !ring && !queue && !host ? 128 : 0) |
-           (host && !ring && !queue ? 64 : 0) | (queue && emit ? 32 : 0) | (ring ? 16 : 0) |
-           (lean && nolb ? 8 : 0) | (lean ? 4 : 0) | (tss ? 2 : 0) | (emit ? 1 : 0);
+// bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
+// upe_gpu_process_host; not ring), bit 6 a header-split batch (upe_gpu_process_split_emit; emit
+// only, not ring or host).
+enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
+       VAR_SPLIT = 64 };
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
+                 bool split = false) {
+    return (split && emit && !ring && !host ? VAR_SPLIT : 0) | (host && !ring ? VAR_HOST : 0) |
+           (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) | (lean ? VAR_LEAN : 0) |
+           (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
 }
 // The instantiated variants (every combination classify_var can return for a launch).
 constexpr bool var_built(int v) {
-    const bool emit = v & 1, lean = v & 4, nolb = v & 8, ring = v & 16, queue = v & 32,
-               host = v & 64, split = v & 128;
+    const bool emit = v & VAR_EMIT, lean = v & VAR_LEAN, nolb = v & VAR_NOLB, ring = v & VAR_RING,
+               host = v & VAR_HOST, split = v & VAR_SPLIT;
     if (nolb && !lean) return false;
-    if (ring) return !split && !queue && !host && emit && lean && !(v & 2);
-    if (queue) return !split && !host && emit;
+    if (ring) return !split && !host && emit && lean && !(v & VAR_TSS);
     if (split) return emit && !host;
     return true;
 }
@@ -2588,8 +2370,9 @@ template <int V>
 const void* classify_fn_of() {
     if constexpr (var_built(V))
         return reinterpret_cast<const void*>(
-            &upe_classify<(V & 2) != 0, (V & 1) != 0, (V & 4) != 0, (V & 8) != 0, (V & 16) != 0,
-                          (V & 32) != 0, (V & 64) != 0, (V & 128) != 0>);
+            &upe_classify<(V & VAR_TSS) != 0, (V & VAR_EMIT) != 0, (V & VAR_LEAN) != 0,
+                          (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0,
+                          (V & VAR_SPLIT) != 0>);
     else
         return nullptr;
 }
@@ -2625,11 +2408,6 @@ uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
     const uint64_t key = (uint64_t)lds << 8 | (uint64_t)var;
     auto it = c->resident.find(key);
     if (it != c->resident.end()) return it->second;
-    // a census counts what an idle chip holds: let an overlapped queue's previous launch finish
-    if (c->q_prev && hipStreamSynchronize(c->q_prev) != hipSuccess) {
-        fail("census: synchronising the previous launch failed");
-        return 0;
-    }
     int per_cu = 0;
     hipError_t e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, classify_fn(var), kBlock, lds);
@@ -2796,7 +2574,6 @@ upe_gpu_ctx_t* upe_gpu_open(int device, size_t rule_capacity) {
         if (const char* v = getenv("UPE_GPU_LB_SPIN")) c->lb_spin = (uint32_t)strtoul(v, nullptr, 10);
         if (const char* v = getenv("UPE_GPU_LB_SYNC")) c->lb_sync = v[0] == '1';
         if (const char* v = getenv("UPE_GPU_NOLB")) c->allow_nolb = v[0] != '0';
-        if (const char* v = getenv("UPE_GPU_HOST_SERIAL")) c->host_serial = atoi(v) != 0;
         if (const char* v = getenv("UPE_GPU_HOST_SLOTS"))
             c->host_slots = std::min(8u, std::max(2u, (uint32_t)strtoul(v, nullptr, 10)));
     }
@@ -2851,7 +2628,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->lens16, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tf4, c->tf6, c->tfs,
+                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs,
                     c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
                     c->hist_part};
@@ -2869,9 +2646,6 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     }
     if (c->s_in) (void)hipStreamSynchronize(c->s_in), (void)hipStreamDestroy(c->s_in);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out), (void)hipStreamDestroy(c->s_out);
-    if (c->q_stream) (void)hipStreamSynchronize(c->q_stream), (void)hipStreamDestroy(c->q_stream);
-    if (c->q_ev) (void)hipEventDestroy(c->q_ev);
-    if (c->sig) (void)hipFree(c->sig);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->agree_h) (void)hipHostFree(c->agree_h);
     delete c;
@@ -2879,8 +2653,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
 
 namespace {
 // Credit the sorted-index totals of the current table to rule_stats[rule_id] (device) and clear
-// them: called before the table changes, so a reload keeps every count (src/main.c:216-282
-// swaps rule_stats with the table; here the counts simply carry over by rule_id).
+// them: called before upe_gpu_load_rules changes the table, so the counts carry over by rule_id
+// (upe_gpu_reload_rules instead starts a fresh rule_stats, as the reference's SIGHUP reload does).
 // Every table size keeps its counts per sorted index: small tables in the per-batch replicated
 // accumulators (acc_stats, added here), mid-size ones in kStatReps replicas (each workgroup's LDS
 // bins) and large ones too (upe_rule_hist).  The host sums the replicas and credits rule_id.
@@ -2920,6 +2694,26 @@ int fold_stats_idx(upe_gpu_ctx* c) {
                       hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(c->stats_idx, 0, E * kStatReps * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats)));
+    return 0;
+}
+
+// rule_stats[0..capacity) as the worker holds them: the per-rule_id array plus the current
+// table's per-sorted-index totals credited to their rule_id (after a device synchronisation).
+int read_rule_stats(upe_gpu_ctx* c, upe_rule_stat_t* rule_stats, size_t capacity) {
+    const size_t k = capacity < c->cap ? capacity : c->cap;
+    memset(rule_stats, 0, capacity * sizeof(upe_rule_stat_t));
+    HIP_TRY(hipMemcpy(rule_stats, c->stats, k * sizeof(upe_rule_stat_t), hipMemcpyDeviceToHost));
+    if (c->stats_idx && !c->rinfo_host.empty()) {
+        const size_t E = 2 * (size_t)c->nrules_pad;
+        std::vector<unsigned long long> idx;
+        if (read_stats_idx(c, idx) != 0) return -1;
+        for (size_t e = 0; e < E; ++e) {
+            const uint32_t rid = (uint32_t)c->rinfo_host[e >> 1].y;
+            if (!idx[e] || rid >= k) continue;
+            if (e & 1) rule_stats[rid].bytes += idx[e];
+            else rule_stats[rid].packets += idx[e];
+        }
+    }
     return 0;
 }
 }  // namespace
@@ -3018,12 +2812,9 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
             out.fp[fbase + t] = tss_tag(tss_hash(k.data(), nw, seed));
             uint4* e = &out.slots[base + t * per];
             const uint32_t act = act_code(rules[idx[slot[t]]].action.type);
-            if (F == 4 && kTssSlot16) {
+            if (F == 4) {
                 const uint32_t v = (idx[slot[t]] + 1u) | act << 22;
                 e[0] = make_uint4(k[0] | (v & 0xFFu), k[1] | ((v >> 8) << 16), k[2], k[3]);
-            } else if (F == 4) {
-                e[0] = make_uint4(k[0], k[1], k[2], k[3]);
-                e[1] = make_uint4(idx[slot[t]], 1u, act, 0u);
             } else {
                 e[0] = make_uint4(k[0], k[1], k[2], k[3]);
                 e[1] = make_uint4(k[4], k[5], k[6], k[7]);
@@ -3156,8 +2947,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
                 if (upload(c->tfs, img)) return -1;
                 c->nfs = (uint32_t)(img.size() / 8);
                 if (upload(c->tg4, f4.groups) || upload(c->tg6, f6.groups) ||
-                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots) ||
-                    upload(c->tf4, f4.fp) || upload(c->tf6, f6.fp))
+                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots))
                     return -1;
                 c->ng4 = (uint32_t)f4.groups.size();
                 c->ng6 = (uint32_t)f6.groups.size();
@@ -3166,6 +2956,44 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         }
     }
     return 0;
+}
+
+// The reference's SIGHUP reload (src/main.c:216-282): the stats thread builds a new table
+// (rule_table_init(1024) + rule_config_load), gives every worker a fresh calloc'd rule_stats of
+// the new table's capacity, swaps w->rt and w->rule_stats between two of the worker's bursts and
+// frees the old ones after a grace period.  The worker's pkts_* counters and its one-entry L1
+// neighbour caches are untouched.  Here: the batches queued so far finish with the old table,
+// their rule_stats (credited to the old rule_ids) are handed back in old_stats if asked for,
+// and the next batch runs with the new table and an all-zero rule_stats[rule_capacity].
+extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
+                                    size_t rule_capacity, upe_rule_stat_t* old_stats,
+                                    size_t old_capacity) {
+    if (!c) return fail("null context");
+    if (rule_capacity == 0 || rule_capacity > (1u << 24)) return fail("rule_capacity must be in [1, 2^24]");
+    if (count > rule_capacity) return fail("rule count exceeds the new capacity");
+    if (count && !rules) return fail("null rules");
+    if (old_capacity && !old_stats) return fail("null old_stats");
+    for (size_t i = 0; i < count; ++i)
+        if (rules[i].rule_id >= rule_capacity) return fail("rule_id >= capacity (rule_stats index)");
+    DEV_SCOPE(c->device);
+    // the batches queued with the old table finish first (on whichever stream they went)
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (old_capacity && read_rule_stats(c, old_stats, old_capacity) != 0) return -1;
+    // a fresh, zeroed rule_stats of the new capacity; the old table's per-index totals dropped
+    unsigned long long* fresh = nullptr;
+    HIP_TRY(hipMalloc(&fresh, rule_capacity * 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(fresh, 0, rule_capacity * 2 * sizeof(unsigned long long)));
+    if (c->stats) (void)hipFree(c->stats);
+    c->stats = fresh;
+    c->cap = rule_capacity;
+    if (c->stats_idx)
+        HIP_TRY(hipMemset(c->stats_idx, 0,
+                          (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats)));
+    c->rinfo_host.clear();   // nothing of the old table is left to credit
+    if (publish(c) != 0) return -1;
+    return upe_gpu_load_rules(c, rules, count);
 }
 
 extern "C" int upe_gpu_rule_index_kind(upe_gpu_ctx_t* c) {
@@ -3357,9 +3185,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             HIP_TRY(hipEventCreate(&e));
             c->ev.push_back(e);
         }
-        // (in an overlapped queue, after the previous launch: the sample spans timing_span
-        // launch-to-launch intervals)
-        HIP_TRY(hipEventRecord(c->ev[c->ev_used], c->q_prev ? c->q_prev : s));
+        HIP_TRY(hipEventRecord(c->ev[c->ev_used], s));
         c->t_left = c->timing_span;
     }
     Args a;
@@ -3382,8 +3208,6 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.tg6 = c->tg6;
     a.tt4 = c->tt4;
     a.tt6 = c->tt6;
-    a.tf4 = c->tf4;
-    a.tf6 = c->tf6;
     a.tfs = reinterpret_cast<const uint4*>(c->tfs);
     a.ng4 = c->ng4;
     a.ng6 = c->ng6;
@@ -3454,16 +3278,16 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.agree_out = c->no_lb ? nullptr : c->agree_d;
     a.launch_tag = c->k + 1;
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
-    bool stamp = ring && ring->done && emit && lean && !c->tss;
-    const bool queue = c->fin_next_flags != 0;   // a launch of upe_gpu_process_queue_emit
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, queue, host, slab != nullptr);
+    // (at most kRingMax batches: one LDS counter each)
+    bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, slab != nullptr);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, queue, host,
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host,
                                       slab != nullptr), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
@@ -3477,8 +3301,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     const uint32_t grid = a.ntiles == 0 ? 1u : a.ntiles < grid_cap ? a.ntiles : grid_cap;
     if (ring && ring->done) {
         HIP_TRY(hipMemsetAsync(ring->done, 0, (n / ring->per) * sizeof(unsigned long long), s));
-        // every workgroup must own the same number of tiles of every batch (at least one), so
-        // that it has at most two batches in flight (kRing's four LDS counters)
+        // every workgroup must own the same number of tiles of every batch (at least one)
         const size_t tpb = (ring->per / 64) / tw;
         if (stamp && (tpb < grid || tpb % grid != 0)) stamp = false;
         if (!stamp) {
@@ -3501,16 +3324,6 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             a.ring_done = ring->done;
             a.ring_t0 = c->ring_wg + nb;
         }
-    }
-    a.fin_flags = c->fin_next_flags;
-    a.fin_wait = c->fin_next_wait;
-    c->fin_next_flags = 0;
-    if (a.fin_flags & 1u) c->fin_total += grid;
-    if (a.fin_flags & 2u) ++c->overlapped;
-    if (a.fin_flags & 4u) {
-        c->start_total += grid;
-        a.start_target = c->start_total;
-        a.sig = c->sig;
     }
     launch_classify(var, grid, lds, s, a);
     HIP_TRY(hipGetLastError());
@@ -3664,10 +3477,9 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         }
     } drain{c};
     const size_t nslots = c->host_slots;
-    // the stream the copies back go to: the copy-out stream (both link directions at once), or
-    // the copy-in stream, one direction at a time
-    const bool serial = c->host_serial < 0 ? false : c->host_serial != 0;
-    hipStream_t s_back = serial ? c->s_in : c->s_out;
+    // copies back on their own stream: both link directions at once (issuing them on the copy-in
+    // stream after the next chunk's copy-in measured slower: B 332-344 vs 480 Mpps in place)
+    hipStream_t s_back = c->s_out;
     const size_t lag = 2;   // emit: chunk k - lag is applied while chunk k is issued
     struct Done {
         size_t s, e, slot;
@@ -3703,28 +3515,22 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
     };
     // a chunk's copy-back (verdicts + records, or verdicts + the rewritten span), once its kernel
     // is queued
-    struct Back {
-        bool pending;
-        size_t s, e, slot;
-        uint64_t lo, wb;
-    } back{false, 0, 0, 0, 0, 0};
-    auto issue_back = [&]() -> int {
-        auto& sb = c->hs[back.slot];
-        const size_t m = back.e - back.s;
-        back.pending = false;
+    auto issue_back = [&](size_t s, size_t e, size_t slot, uint64_t lo, uint64_t wb) -> int {
+        auto& sb = c->hs[slot];
+        const size_t m = e - s;
         HIP_TRY(hipStreamWaitEvent(s_back, sb.k_done, 0));
-        HIP_TRY(hipMemcpyAsync(h_verdict + back.s, sb.verdict, m * sizeof(uint32_t),
+        HIP_TRY(hipMemcpyAsync(h_verdict + s, sb.verdict, m * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, s_back));
         if (emit)
-            HIP_TRY(hipMemcpyAsync(h_hdr + back.s, sb.hdr, m * sizeof(upe_hdr_rec_t),
+            HIP_TRY(hipMemcpyAsync(h_hdr + s, sb.hdr, m * sizeof(upe_hdr_rec_t),
                                    hipMemcpyDeviceToHost, s_back));
         else
-            HIP_TRY(hipMemcpyAsync(h_frames + back.lo, sb.frames, (size_t)(back.wb - back.lo),
+            HIP_TRY(hipMemcpyAsync(h_frames + lo, sb.frames, (size_t)(wb - lo),
                                    hipMemcpyDeviceToHost, s_back));
         HIP_TRY(hipEventRecord(sb.out_done, s_back));
         sb.busy = true;
-        sb.lo = back.lo;
-        sb.wb = back.wb;
+        sb.lo = lo;
+        sb.wb = wb;
         return 0;
     };
     size_t k = 0;
@@ -3780,9 +3586,6 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         // landed: its own copy-back rewrites its whole span, and would otherwise put back the
         // earlier chunk's frames as they were before they were processed.  (Emit mode copies
         // no frame bytes back.)
-        // (a copy-back still deferred, serial mode, goes first if this chunk's bytes interleave
-        // with its chunk's: on the same stream, it then lands before this chunk is read)
-        if (back.pending && !emit && back.lo < hi && lo < back.wb && issue_back() != 0) return -1;
         if (!emit)
             for (auto& other : c->hs)
                 if (&other != &sl && other.busy && other.lo < hi && lo < other.wb)
@@ -3800,14 +3603,9 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
                          nullptr, nullptr, true) != 0)
             return -1;
         HIP_TRY(hipEventRecord(sl.k_done, c->stream));
-        // serial mode: this chunk's copy-back is issued after the next chunk's copy-in, so that
-        // the copy-in stream never idles while a kernel runs
-        if (back.pending && issue_back() != 0) return -1;
-        back = Back{true, s, e, si, lo, wb};
-        if (!serial && issue_back() != 0) return -1;
+        if (issue_back(s, e, si, lo, wb) != 0) return -1;
         if (emit) pending.push_back(Done{s, e, si, lo});
     }
-    if (back.pending && issue_back() != 0) return -1;
     for (const Done& d : pending)
         if (finish(d) != 0) return -1;
     HIP_TRY(hipStreamSynchronize(s_back));
@@ -3919,68 +3717,15 @@ int upe_gpu_process_queue_emit(upe_gpu_ctx_t* c, const upe_gpu_batch_t* batches,
                                void* stream) {
     if (!c) return fail("null context");
     if (count && !batches) return fail("null batch list");
-    DEV_SCOPE(c->device);
-    if (c->overlap < 0) {
-        const char* e = getenv("UPE_GPU_OVERLAP");
-        int can = 0;
-        // opt-in: measured slower than sequential launches on MI355X
-        c->overlap = (e && atoi(e) != 0) &&
-                     hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue,
-                                           c->device) == hipSuccess && can;
-    }
-    // Overlap needs no group-by launches after each classify (they would read the shared length
-    // array while the next launch writes it) and one launch per batch.
-    bool ov = c->overlap == 1 && count > 1 && c->nrules_pad <= (uint32_t)kLdsStatsMax;
-    for (size_t k = 0; ov && k < count; ++k) ov = batches[k].n <= kMaxLaunch;
-    if (!ov) {
-        for (size_t k = 0; k < count; ++k)
-            if (process_impl(c, batches[k].frames, batches[k].desc, batches[k].verdict, nullptr,
-                             batches[k].hdr, batches[k].n, stream) != 0)
-                return -1;
-        return 0;
-    }
-    hipStream_t s0 = pick(c, stream);
-    if (!c->q_stream) HIP_TRY(hipStreamCreateWithFlags(&c->q_stream, hipStreamNonBlocking));
-    if (!c->q_ev) HIP_TRY(hipEventCreateWithFlags(&c->q_ev, hipEventDisableTiming));
-    if (!c->sig) {
-        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), 8, hipMallocSignalMemory));
-        HIP_TRY(hipMemset(c->sig, 0, 8));
-    }
-    // both streams after everything queued so far on the context
-    if (order_on(c, s0) != 0) return -1;
-    HIP_TRY(hipEventRecord(c->q_ev, s0));
-    HIP_TRY(hipStreamWaitEvent(c->q_stream, c->q_ev, 0));
-    hipStream_t prev = nullptr;
-    int rc = 0;
-    for (size_t k = 0; k < count && rc == 0; ++k) {
-        hipStream_t sk = (k & 1) ? c->q_stream : s0;
-        if (k && !(UPE_DIAG_Q_NOWAIT && getenv("UPE_GPU_DIAG_NO_GATE"))) {
-            // not before every workgroup of the previous launch is resident (its last one to
-            // start stores the previous launch's tag, c->k, into the signal word)
-            const hipError_t e = hipStreamWaitValue32(sk, c->sig, (uint32_t)c->k,
-                                                      hipStreamWaitValueGte, 0xFFFFFFFFu);
-            if (e != hipSuccess) {
-                rc = fail(std::string("hipStreamWaitValue32: ") + hipGetErrorString(e));
-                break;
-            }
-        }
-        c->fin_next_flags = 1u | 4u | (k ? 2u : 0u);
-        c->fin_next_wait = c->fin_total;
-        c->q_prev = prev;
-        c->last_stream = sk;   // ordered by the wait above, not by order_on's event
-        rc = process_impl(c, batches[k].frames, batches[k].desc, batches[k].verdict, nullptr,
-                          batches[k].hdr, batches[k].n, sk);
-        prev = sk;
-    }
-    c->q_prev = nullptr;
-    c->fin_next_flags = 0;
-    // the caller's stream after the queue's last launch
-    if (prev && prev != s0) {
-        HIP_TRY(hipEventRecord(c->q_ev, prev));
-        HIP_TRY(hipStreamWaitEvent(s0, c->q_ev, 0));
-    }
-    c->last_stream = s0;
-    return rc;
+    // one launch after another (overlapping consecutive launches on two streams measured slower
+    // on MI355X: DESIGN.md §8, round 3); every batch is checked before any is queued
+    for (size_t k = 0; k < count; ++k)
+        if (batches[k].n && !batches[k].hdr) return fail("null header records in a queued batch");
+    for (size_t k = 0; k < count; ++k)
+        if (process_impl(c, batches[k].frames, batches[k].desc, batches[k].verdict, nullptr,
+                         batches[k].hdr, batches[k].n, stream) != 0)
+            return -1;
+    return 0;
 }
 
 int upe_gpu_process_batches_emit(upe_gpu_ctx_t* c, uint8_t* const* d_frames_list,
@@ -4230,7 +3975,6 @@ int upe_gpu_launch_info(upe_gpu_ctx_t* c, upe_launch_info_t* info) {
     HIP_TRY(hipDeviceSynchronize());
     memset(info, 0, sizeof *info);
     info->launches = c->k;
-    info->overlapped = c->overlapped;
     if (c->k == 0 || c->last_var < 0) return 0;
     info->variant = (uint32_t)c->last_var;
     info->grid = c->last_grid;
@@ -4258,22 +4002,7 @@ int upe_gpu_get_stats(upe_gpu_ctx_t* c, upe_counters_t* counters, upe_rule_stat_
                 for (int j = 0; j < 7; ++j) dst[1 + j] += b.cnt[r][j];
         }
     }
-    if (rule_stats) {
-        const size_t k = capacity < c->cap ? capacity : c->cap;
-        HIP_TRY(hipMemcpy(rule_stats, c->stats, k * sizeof(upe_rule_stat_t), hipMemcpyDeviceToHost));
-        if (c->stats_idx && !c->rinfo_host.empty()) {
-            // this table's counts are kept per sorted index: credit them to rule_id
-            const size_t E = 2 * (size_t)c->nrules_pad;
-            std::vector<unsigned long long> idx;
-            if (read_stats_idx(c, idx) != 0) return -1;
-            for (size_t e = 0; e < E; ++e) {
-                const uint32_t rid = (uint32_t)c->rinfo_host[e >> 1].y;
-                if (!idx[e] || rid >= k) continue;
-                if (e & 1) rule_stats[rid].bytes += idx[e];
-                else rule_stats[rid].packets += idx[e];
-            }
-        }
-    }
+    if (rule_stats && read_rule_stats(c, rule_stats, capacity) != 0) return -1;
     return 0;
 }
 

@@ -23,8 +23,11 @@ LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")  # override: diagnostic builds only
 
 
-VAR_NOLB = 8   # launch_info variant bit: the kernel without look-back
-VAR_HOST = 64  # launch_info variant bit: a host path's launch (mapped host memory, host round trip)
+# launch_info variant bits (upe_gpu.hip classify_var)
+VAR_NOLB = 8    # the kernel without look-back
+VAR_RING = 16   # a ring launch whose batches are stamped
+VAR_HOST = 32   # a host path's launch (mapped host memory, host round trip)
+VAR_SPLIT = 64  # a header-split batch
 
 
 # upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
@@ -57,6 +60,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_open": (P, [I, SZ]),
         "upe_gpu_close": (None, [P]),
         "upe_gpu_load_rules": (I, [P, P, SZ]),
+        "upe_gpu_reload_rules": (I, [P, P, SZ, SZ, P, SZ]),
         "upe_gpu_load_neigh": (I, [P, P, SZ, P, SZ]),
         "upe_gpu_rule_index_kind": (I, [P]),
         "upe_gpu_set_port": (I, [P, P, ctypes.c_uint32]),
@@ -115,7 +119,7 @@ LIB = _load()
 # every symbol include/upe_gpu.h declares (checked by tests/test_abi.py)
 EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", "upe_gpu_pin_self",
             "upe_gpu_open", "upe_gpu_close",
-            "upe_gpu_load_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
+            "upe_gpu_load_rules", "upe_gpu_reload_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
             "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
             "upe_gpu_launch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
@@ -207,6 +211,21 @@ class GpuWorker:
         r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
         _check(LIB.upe_gpu_load_rules(self._ctx, _np_ptr(r) if len(r) else None, len(r)),
                "upe_gpu_load_rules")
+
+    def reload_rules(self, rules_sorted: np.ndarray, capacity: int | None = None,
+                     want_old: bool = True):
+        """upe_gpu_reload_rules: the SIGHUP reload (src/main.c:216-282) — new table, fresh zero
+        rule_stats of `capacity` entries (default: unchanged), counters and L1 kept.  Returns the
+        old rule_stats (old capacity) when want_old."""
+        cap = self.capacity if capacity is None else int(capacity)
+        r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
+        old = np.zeros(self.capacity, RULE_STAT_DTYPE) if want_old else None
+        _check(LIB.upe_gpu_reload_rules(self._ctx, _np_ptr(r) if len(r) else None, len(r), cap,
+                                        _np_ptr(old) if want_old else None,
+                                        self.capacity if want_old else 0),
+               "upe_gpu_reload_rules")
+        self.capacity = cap
+        return old
 
     def rule_index_kind(self) -> int:
         """0: linear scan, 1: tuple-space index."""

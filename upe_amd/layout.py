@@ -55,8 +55,9 @@ L1_DTYPE = np.dtype(
 BATCH_INFO_DTYPE = np.dtype([("counters", COUNTERS_DTYPE), ("n_ctrl", "<u8"),
                              ("first_ctrl", "<u8")])
 # upe_launch_info_t (include/upe_gpu.h)
-LAUNCH_INFO_DTYPE = np.dtype([("variant", "<u4"), ("grid", "<u4"), ("deferred", "<u4"),
-                              ("overlapped", "<u4"), ("launches", "<u8")])
+LAUNCH_INFO_DTYPE = np.dtype({"names": ["variant", "grid", "deferred", "launches"],
+                              "formats": ["<u4", "<u4", "<u4", "<u8"],
+                              "offsets": [0, 4, 8, 16], "itemsize": 24})
 
 # verdict word (include/upe_gpu.h)
 V_DROP_PARSE, V_DROP_NOMATCH, V_DROP_RULE, V_DROP_TTL, V_FWD, V_CONSUMED, V_DROP_ACTION = range(7)
