@@ -170,11 +170,14 @@ def pmc_traffic(config: str, packets: int, mode: str):
     return d["traffic_bytes_per_launch"] if d.get("packets") == packets else None
 
 
-def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
+def cpu_baseline(wl, threads: int, local: list | None = None, numa_all: bool = True) -> dict:
     """The reference worker timed on this host: one shard and calloc'd worker_t per thread, each
     pinned to its own core — the GPU's NUMA-local cores first (`local`), then the rest of the
     affinity mask.  `threads` is this job's CPU share (16 per GPU on the GPU box; the machine's
-    other cores belong to other jobs), reported with the spread of the passes."""
+    other cores belong to other jobs), reported with the spread of the passes.  numa_all: also
+    every NUMA-local core of the GPU (the node's whole CPU side, busy with other jobs or not), on
+    a 4M-packet sample of the same workload so that each thread's shard stays in the tens of
+    thousands of packets."""
     import oracle
 
     sample = f"{wl.n} packets of the same workload, median of 9 passes after 1 warm-up"
@@ -193,7 +196,23 @@ def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
                      if l.startswith("model name")][0]
         except Exception:
             model = "unknown"
+        numa = None
+        loc = [c for c in (local or []) if c in allowed]
+        if numa_all and len(loc) > len(cpus):
+            from upe_amd import synth
+
+            big = synth.config_b(n=1 << 22, seed=2)
+            ra = []
+            va = oracle.time_reference(big, threads=len(loc), cpus=loc, reps=9, rates=ra)
+            numa = {"value": round(va / 1e6, 3), "unit": "Mpps", "cores": len(loc),
+                    "spread": {"min": round(ra[0] / 1e6, 3), "median": round(va / 1e6, 3),
+                               "max": round(ra[-1] / 1e6, 3), "passes": len(ra)},
+                    "sample": f"{big.n} packets of the same workload (config B, seed 2) split over "
+                              "every CPU of the GPU's NUMA node in this process's affinity, one "
+                              "pinned thread each; median of 9 passes after 1 warm-up",
+                    "note": "the node's other jobs share these cores: the spread says how much"}
         return {"value": round(vn / 1e6, 3), "unit": "Mpps", "cores": len(cpus),
+                "numa_local_all": numa,
                 "kind": "reference", "single_core_value": round(v1 / 1e6, 3),
                 "spread": {"min": round(rn[0] / 1e6, 3), "median": round(vn / 1e6, 3),
                            "max": round(rn[-1] / 1e6, 3), "passes": len(rn),
@@ -213,6 +232,51 @@ def cpu_baseline(wl, threads: int, local: list | None = None) -> dict:
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(wl.n / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
             "sample": sample}
+
+
+def dropin_pipeline(local: list | None, seconds: float = 2.0, device: int = 0) -> dict | None:
+    """Part of the cpu_baseline leg (it runs the reference's own pipeline code, oracle/_ref): the
+    reference's throughput benchmark (tests/benchmark_throughput.c:87-116,188-238,303-375: a
+    synthetic-NIC producer thread building 64 B TCP packets in the reference pktbuf pool and
+    pushing bursts of 32 round robin into the reference SPSC rings, workers popping them, TX
+    stubbed; consumer Mpps = packets the workers popped / the producer's time) with the
+    reference's own worker threads (src/worker.c worker_main) and with GPU workers — the product
+    loop upe_gpu_worker_run bound to the same worker_t (oracle/dropin_worker.c) — on this GPU.
+    Threads pinned to the GPU's NUMA-local CPUs (producer first).  Not `value`."""
+    import ctypes
+
+    import oracle
+
+    so = os.path.join(os.path.dirname(oracle.__file__), "_ref", "libupe_dropin.so")
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    P, SZ, I, D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
+    lib.upe_dropin_bench.restype = I
+    lib.upe_dropin_bench.argtypes = [I, I, I, I, SZ, SZ, I, I, D, D, SZ, P, P]
+    cpus_all = [c for c in (local or []) if c in ALLOWED_CPUS] or ALLOWED_CPUS
+    legs = []
+    for pool, ring in ((8192, 1024), (262144, 32768)):
+        for gpu, mapped, workers in ((0, 0, 1), (0, 0, 4), (1, 1, 1), (1, 0, 1)):
+            cpus = (ctypes.c_int * (1 + workers))(*[cpus_all[k % len(cpus_all)]
+                                                    for k in range(1 + workers)])
+            out = (ctypes.c_double * 5)()
+            rc = lib.upe_dropin_bench(gpu, mapped, workers, device, pool, ring, 32, 64, 0.5,
+                                      seconds, 65536, cpus, out)
+            legs.append({"workers": (f"{workers} GPU worker(s), " +
+                                     ("pktbufs classified in the registered pool (mapped)"
+                                      if mapped else "header windows via the DMA round trip"))
+                         if gpu else f"{workers} reference worker thread(s) (src/worker.c)",
+                         "pool": pool, "ring": ring, "rc": rc,
+                         "consumer_mpps": round(out[0], 2), "producer_mpps": round(out[1], 2),
+                         "ring_full_events": int(out[2]), "seconds": round(out[3], 3)})
+    return {"legs": legs, "packet": "64 B Eth/IPv4/TCP 10.128.0.1:45000 -> 10.128.0.2:80, "
+                                     "1 TCP FWD rule, 1 ARP entry (the reference bench's setup)",
+            "what": "the reference's e2e throughput benchmark (one producer thread -> SPSC rings "
+                    "-> workers -> stubbed TX), consumer Mpps = worker pkts_in / producer time; "
+                    "pool / ring = the reference defaults (8192 / 1024) and a GPU-sized pair; "
+                    f"{seconds} s after 0.5 s warm-up per leg; the single producer thread bounds "
+                    "every leg (producer_mpps)"}
 
 
 def host_roundtrip(worker, wl, reps: int, chunk: int, windows: bool, apply_threads=None) -> dict:
@@ -361,7 +425,8 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
     total = float(shard.sum_over_ranks([n * steps], dist, dev)[0])
     v = verdict.cpu().numpy().view(np.uint32).copy()
-    cms, _, launches = worker.timing_read()
+    cms, gms, launches = worker.timing_read()
+    cms += gms
     worker.close()
     del pool, desc, verdict, hdr
     if split:
@@ -382,6 +447,110 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                       "packed frames (upe_gpu_process_emit)",
             "what": f"all ranks at once after the main region, {copies} distinct batch copies "
                     "cycled, same timing protocol as value (barrier, max over ranks)"}
+
+
+VALU_PEAK_G = 1024 * 2.4 / 2   # G wave64 VALU instructions/s: 1024 SIMD-32s, one per 2 cycles
+
+
+def pmc_valu(config: str, packets: int, mode: str = "emit"):
+    """The classify kernel's VALU counts per launch from the committed PMC passes
+    (profiles/pmc_config<X>[_emit]_valu.json, tools/pmc_run.sh + tools/pmc_valu.py), or None."""
+    path = os.path.join(ROOT, "profiles",
+                        f"pmc_config{config}{'_emit' if mode == 'emit' else ''}_valu.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return d if d.get("packets") == packets else None
+
+
+def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: int = 8) -> dict:
+    """BASELINE configs[3] (16M packets: IPv4 options, TCP data offsets, 10 % malformed, v4 / v6
+    mixed per wave; 64k rules, the tuple-space index) timed after the main region with the same
+    protocol (emit mode, distinct batch copies cycled, wall time over `steps` launches; HIP
+    events around every launch split classify and the rule_stats group-by).  Its roofline is
+    the VALU issue rate (the rule work, not bytes, was expected to bound it): the
+    classify kernel's VALU wave-instructions per launch (committed PMC, tools/pmc_valu.py) over
+    the live classify time, against 1024 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz; the
+    HBM fractions follow.  Not `value`."""
+    from upe_amd import gpu, synth
+
+    t_gen = time.perf_counter()
+    wl = synth.config_d()
+    t_gen = time.perf_counter() - t_gen
+    n = wl.n
+    worker = gpu.GpuWorker(local, wl.capacity)
+    worker.configure(wl)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    fbytes = int(wl.frames.nbytes)
+    stride = (fbytes + 255) // 256 * 256
+    copies = max(2, min(steps + warmup, copies_cap))
+    pristine = torch.from_numpy(wl.frames).to(dev)
+    pool = torch.empty(copies * stride, dtype=torch.uint8, device=dev)
+    for c in range(copies):
+        pool[c * stride: c * stride + fbytes].copy_(pristine)
+    del pristine
+    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    base = pool.data_ptr()
+    ptrs = [base + (k % copies) * stride for k in range(warmup + steps)]
+    worker.process_batches_emit(ptrs[:warmup], desc, verdict, hdr, n, sh)
+    torch.cuda.synchronize(dev)
+    timed = gpu.GpuWorker.frames_list(ptrs[warmup:])
+    worker.timing_span(1, 1)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    worker.process_batches_emit(timed, desc, verdict, hdr, n, sh)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    v = verdict.cpu().numpy().view(np.uint32).copy()
+    cms, gms, launches = worker.timing_read()
+    kind = worker.rule_index_kind()
+    worker.close()
+    del pool, desc, verdict, hdr
+    classify_s = cms / launches / 1e3
+    step_s = (cms + gms) / launches / 1e3
+    bpp = algorithmic_bytes(wl, v, emit=True)
+    traffic = pmc_traffic("D", n, "emit")
+    pv = pmc_valu("D", n, "emit")
+    roof = {"bound": "valu", "unit": "G VALU wave-instructions/s", "peak": round(VALU_PEAK_G, 1),
+            "kernel": "upe_classify (tuple-space variant)", "classify_ms": round(classify_s * 1e3, 4),
+            "group_by_ms": round(gms / launches, 4), "event_samples": int(launches)}
+    if pv:
+        ach = pv["sq_insts_valu"] / classify_s / 1e9
+        roof.update({"achieved": round(ach, 1), "frac": round(ach / VALU_PEAK_G, 4),
+                     "valu_insts_per_launch": pv["sq_insts_valu"],
+                     "frac_pmc_cycles": round(pv["valu_frac"], 4),
+                     "valu_lane_insts_per_packet": round(pv["valu_insts_per_packet"], 1),
+                     "source": "VALU instructions: profiles/pmc_configD_emit_valu.json (rocprofv3 "
+                               "SQ_INSTS_VALU per classify launch); time: this run's HIP events; "
+                               "frac_pmc_cycles: the PMC run's own GRBM_GUI_ACTIVE cycles"})
+    else:
+        roof.update({"achieved": None, "frac": None,
+                     "source": "no committed VALU PMC summary for this batch size"})
+    hbm_alg = float(bpp.sum()) / step_s / 1e9
+    roof["hbm"] = {"achieved": round(hbm_alg, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                   "frac": round(hbm_alg / HBM_PEAK_GBPS, 4),
+                   "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
+                   "basis": "algorithmic bytes per step / step kernel time (classify + group-by)"}
+    if traffic:
+        roof["hbm"]["traffic"] = traffic
+        roof["hbm"]["traffic_frac"] = round(traffic / classify_s / 1e9 / HBM_PEAK_GBPS, 4)
+        roof["hbm"]["traffic_note"] = ("bytes requested past L2 per classify launch (PMC, "
+                                       "profiles/pmc_configD_emit.json; Infinity-Cache hits "
+                                       "included) / classify time")
+    return {"workload": WORKLOADS["D"] + f", {n} packets per step", "value": round(n * steps / elapsed / 1e6, 2),
+            "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps,
+            "rule_index": "tuple space" if kind == 1 else "linear scan",
+            "roofline": roof,
+            "rule_scan_equiv": {"evals_per_batch": rule_evals(wl, v),
+                                "T_evals_per_s": round(rule_evals(wl, v) * steps / elapsed / 1e12, 1),
+                                "what": "rule tests the reference's linear scan would make "
+                                        "(src/rule_table.c:163-176) / wall time: an equivalence, "
+                                        "not the work the tuple-space probes do"},
+            "generation_s": round(t_gen, 1),
+            "what": f"rank 0 at N=1, after the main region; {copies} distinct 2 GB batch copies "
+                    "cycled; emit mode"}
 
 
 def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
@@ -446,6 +615,9 @@ def main() -> None:
                     help="CPU baseline threads: this job's CPU share on the GPU box (16 per GPU; "
                          "the other cores of the machine run other jobs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropin-seconds", type=float, default=2.0,
+                    help="per leg of the reference pipeline benchmark with reference and GPU "
+                         "workers (part of the cpu_baseline leg; 0 skips it)")
     ap.add_argument("--max-copies", type=int, default=1024)
     ap.add_argument("--host-reps", type=int, default=5,
                     help="passes of the host round-trip leg (pinned host batch -> H2D -> "
@@ -478,6 +650,9 @@ def main() -> None:
     ap.add_argument("--imix-split", type=int, default=1,
                     help="1: also time the IMIX leg as header-split batches "
                          "(upe_gpu_process_split_emit), reported as \"imix_split\"")
+    ap.add_argument("--config-d-steps", type=int, default=20,
+                    help="timed steps of the config D leg (16M packets, 64k rules; N=1 config B "
+                         "runs; 0 skips it)")
     ap.add_argument("--ring", type=int, default=16,
                     help="batches per launch of the ring leg (config B; 0 skips it)")
     args = ap.parse_args()
@@ -610,7 +785,8 @@ def main() -> None:
         steps(args.warmup, args.steps, om)
         torch.cuda.synchronize(dev)
         tb = time.perf_counter()
-        oc_ms, _, ol = worker.timing_read()
+        oc_ms, og_ms, ol = worker.timing_read()
+        oc_ms += og_ms
         worker.timing_enable(False)
         other = {"mode": om, "value": round(n * args.steps / (tb - ta) / 1e6, 2), "unit": "Mpps",
                  "ms_per_step": round((tb - ta) / args.steps * 1e3, 5),
@@ -631,6 +807,9 @@ def main() -> None:
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
     probe = hbm_probe(torch, dev) if rank == 0 and not args.no_hbm_probe else None
+    dleg = None
+    if args.config == "B" and world == 1 and args.config_d_steps > 0 and not args.packets:
+        dleg = config_d_leg(torch, dev, local, args.config_d_steps, 3)
 
     # host round trip (not `value`): every rank at once, as the GPUs of a node would run it
     worker.reset_stats()
@@ -672,7 +851,9 @@ def main() -> None:
         bpp = algorithmic_bytes(wl, v_first, emit=args.mode == "emit")
         traffic = pmc_traffic(args.config, n, args.mode)
         bytes_per_launch = float(bpp.sum())
-        kern_s = classify_ms / launches / 1e3 if launches else float("nan")
+        # a step's kernels: the classify launch plus (tables over 4096 rules) the rule_stats
+        # group-by; finalize_ms is the group-by's share (0 for smaller tables)
+        kern_s = (classify_ms + finalize_ms) / launches / 1e3 if launches else float("nan")
         achieved = bytes_per_launch / kern_s / 1e9
         ms_step = elapsed / args.steps * 1e3
         out = {
@@ -709,7 +890,8 @@ def main() -> None:
                                    "PMC, 2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
                 "kernel": "upe_classify",
                 "kernel_ms": round(kern_s * 1e3, 5),
-                "finalize_ms": round(finalize_ms / max(launches, 1), 5),
+                "classify_ms": round(classify_ms / max(launches, 1), 5),
+                "group_by_ms": round(finalize_ms / max(launches, 1), 5),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "algorithmic_bytes_per_packet": round(bytes_per_launch / n, 2),
                 "kernel_mpps": round(n / kern_s / 1e6, 1),
@@ -734,6 +916,8 @@ def main() -> None:
             out["imix_split"] = imix_split
         if ring:
             out["ring"] = ring
+        if dleg:
+            out["config_d"] = dleg
         if shared:
             out["workers_sharing_gpu"] = shared
         def host_line(h, what):
@@ -787,6 +971,10 @@ def main() -> None:
             # config A is the reference's one-worker pcap replay: time it on one core
             out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads,
                                                local_cpus)
+            if args.config == "B" and args.dropin_seconds > 0:
+                dp = dropin_pipeline(local_cpus, args.dropin_seconds, local)
+                if dp:
+                    out["dropin_pipeline"] = dp
         print(json.dumps(out), flush=True)
     worker.close()
     if dist:

@@ -355,6 +355,71 @@ int upe_tx_flush(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t
                  size_t n, size_t burst, upe_tx_batch_fn send, void *user, uint64_t *forwarded,
                  uint64_t *dropped);
 
+/* ------------------------------------------------------------------------------------------ */
+/* The GPU-backed worker loop (upe_amd/csrc/upe_worker.c, C)                                   */
+/* ------------------------------------------------------------------------------------------ */
+/* What the loop needs from the program around it: the callees of reference worker_main /
+ * process_packet (SURVEY.md §8(b) "Callees"), as callbacks with a user pointer first.  A packet
+ * buffer is an opaque handle (a pktbuf_t *). */
+typedef struct upe_worker_ops {
+    /* ring_pop_burst (src/ring.c:53): up to `max` handles into bufs, returns how many */
+    unsigned (*pop_burst)(void *user, void **bufs, unsigned max);
+    /* g_stop (src/worker.c:18), read only when the ring is empty, as src/worker.c:270-273 */
+    int (*stop)(void *user);
+    /* a handle's frame: b->data and b->len (include/pktbuf.h:10-14) */
+    uint8_t *(*data)(void *user, void *buf);
+    size_t (*len)(void *user, void *buf);
+    /* pktbuf_free (src/pktbuf.c:324) */
+    void (*free_buf)(void *user, void *buf);
+    /* tx_send / tx_send_batch (src/tx_afpacket.c:60-118) */
+    int (*tx_send)(void *user, const uint8_t *frame, size_t len);
+    int (*tx_send_batch)(void *user, const uint8_t *const *frames, const size_t *lens, int count);
+    /* handle_control_packet's table writes (src/worker.c:30-39, 64-95): arp_update(ip host
+     * order, mac), ndp_update(ip, mac); then the loop calls load_neigh so that the next packet
+     * sees the write: the callee uploads the tables (upe_gpu_load_neigh under its locks) */
+    void (*arp_update)(void *user, uint32_t ip, const uint8_t mac[6]);
+    void (*ndp_update)(void *user, const uint8_t ip[16], const uint8_t mac[6]);
+    int (*load_neigh)(void *user, upe_gpu_ctx_t *ctx);
+    /* optional: polled after every pop; nonzero = the program changed something the context
+     * holds (a SIGHUP rule swap, src/main.c:258-265; neighbour expiry, src/main.c:205-214): the
+     * loop finishes the packets popped before with the old state, then calls sync(), which
+     * makes the change (upe_gpu_reload_rules, upe_gpu_load_neigh), and classifies the burst just
+     * popped with the new state.  A nonzero return of sync() ends the loop with -1. */
+    int (*poll)(void *user);
+    int (*sync)(void *user, upe_gpu_ctx_t *ctx);
+    /* optional: after every GPU batch, the loop's counters so far (the worker_t fields the stats
+     * thread reads, src/main.c:284-315: pkts_in, pkts_parsed, pkts_matched, pkts_forwarded,
+     * pkts_dropped; the rest as upe_counters_t defines them) */
+    void (*publish)(void *user, upe_gpu_ctx_t *ctx, const upe_counters_t *counters);
+} upe_worker_ops_t;
+
+typedef struct {
+    size_t batch;       /* most packets per GPU batch (0 = 65536) */
+    unsigned burst;     /* most handles per pop (0 = 32, WORKER_BURST_SIZE; at most 64) */
+    /* NULL: each packet's first UPE_HDR_WINDOW bytes are copied into pinned staging and the batch
+     * goes through upe_gpu_process_host_emit (DMA round trip; records applied to the buffers on
+     * return).  Non-NULL: every buffer's frame lies at pool_base + a multiple of 16, inside
+     * memory registered with upe_gpu_host_register (e.g. the reference's pktbuf pool), and each
+     * batch is classified where it lies by upe_gpu_process_mapped (nothing copied). */
+    uint8_t *pool_base;
+    unsigned idle_ns;   /* sleep when the ring is empty and nothing is held (0 = 1000, as
+                           src/worker.c:274-277) */
+} upe_worker_cfg_t;
+
+/* The GPU-backed replacement of worker_main (reference src/worker.c:255-307), on the calling
+ * thread, until the ring is empty with ops->stop() set.  Pops bursts and gathers them into GPU
+ * batches, classified by the context's tables; a batch is cut after every packet that writes a
+ * neighbour table (ARP, NS/NA), whose write is applied through ops before the next packet is
+ * classified, and also run at once whenever the ring is empty.  Then, per popped burst and in
+ * packet order, exactly the calls worker_main makes: tx_send of each answered ARP request,
+ * free_buf of each dropped or consumed packet (pkts_dropped += 1 for a drop), and one
+ * tx_send_batch of the burst's forwarded frames (rewritten as process_packet leaves them) with
+ * pkts_forwarded += sent, pkts_dropped += count - sent, and free_buf of each.  *counters
+ * (optional) receives the loop's counters at the end (they start from zero).  0, or -1 on a
+ * GPU, callback or argument error (upe_gpu_last_error()). */
+int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *user,
+                       const upe_worker_cfg_t *cfg, upe_counters_t *counters);
+
 /* Pinned (page-locked) host memory for upe_gpu_process_host() batches; the GPU can also read and
  * write it directly (upe_gpu_process_mapped). */
 void *upe_gpu_host_alloc(size_t bytes);
@@ -483,7 +548,9 @@ int upe_gpu_reset_stats(upe_gpu_ctx_t *ctx);
  * event pair brackets `span` consecutive calls instead of one, so the events' own latency is
  * spread over `span` launches (the time then includes the gaps between those launches).
  * upe_gpu_timing_read() synchronises and returns the summed time (ms) of the closed samples and
- * the number of calls they cover (finalize_ms is 0: the fold runs inside the classify launch). */
+ * the number of calls they cover: classify_ms up to the end of each sample's last classify
+ * launch, finalize_ms from there to the end of its rule_stats group-by (0 for tables of up to
+ * 4096 rules, which have none). */
 int upe_gpu_timing_enable(upe_gpu_ctx_t *ctx, int enable);
 int upe_gpu_timing_span(upe_gpu_ctx_t *ctx, int every, int span);
 int upe_gpu_timing_read(upe_gpu_ctx_t *ctx, double *classify_ms, double *finalize_ms,

@@ -1,31 +1,36 @@
 /*
- * oracle/dropin_worker.c — the MI355X path dropped into the REFERENCE pipeline.
+ * oracle/dropin_worker.c — the MI355X worker loop dropped into the REFERENCE pipeline
+ * (INTEGRATION.md §1).
  *
  * TEST INFRASTRUCTURE ONLY.  Built by oracle/Makefile against the reference's own headers and
- * sources where they lie (ring, pktbuf pool, rule table, neighbour tables, worker_init), into
+ * sources where they lie (ring, pktbuf pool, rule table, neighbour tables, worker.c), into
  * oracle/_ref/libupe_dropin.so (git-ignored), linked to this repo's libupe_gpu.so.
  *
- * What it shows: a reference worker_t, fed through the reference SPSC ring by an RX-like
- * producer thread exactly as src/rx_pcap.c feeds it (pktbuf_alloc, memcpy, ring_push_burst),
- * runs a GPU-backed worker loop instead of src/worker.c:255-307 — ring_pop_burst bursts
- * aggregated into a pinned batch of header windows, one upe_gpu_process_host() per batch (or, in
- * mapped mode, upe_dropin_set_mapped(1): the pool registered once with upe_gpu_host_register and
- * each batch's pktbufs classified where they lie by upe_gpu_process_mapped, nothing copied) (cut
- * after every packet that writes a neighbour table, whose write is then applied with the
- * reference's own arp_update / ndp_update and the snapshot re-uploaded), then the reference's TX
- * accounting (tx_send_batch, pkts_forwarded / pkts_dropped, pktbuf_free, tx_send of ARP
- * replies) — and ends with the same counters and rule_stats in the same worker_t fields the
- * reference's stats thread reads (src/main.c:293-315).  tests/test_gpu_dropin.py compares
- * them, every packet's bytes and the final neighbour tables with the reference worker itself
- * (oracle/_ref/libupe_ref.so) on the same packets, control packets included.
+ * The first part is the binding a maintainer adds to the reference (INTEGRATION.md §1 shows it):
+ * the callbacks of upe_gpu_worker_run (include/upe_gpu.h, the product loop in
+ * upe_amd/csrc/upe_worker.c) over a reference worker_t — ring_pop_burst on its rx_ring,
+ * pktbuf_t data / len / pktbuf_free, tx_send / tx_send_batch on its tx, arp_update / ndp_update
+ * on its tables, the SIGHUP rule swap picked up between bursts (src/main.c:258-265), and the
+ * counters and rule_stats published into the worker_t fields the stats thread reads
+ * (src/main.c:284-315).  gpu_worker_start() is the GPU counterpart of worker_start().
+ *
+ * The rest drives it: upe_dropin_run() feeds a stream through an RX-like producer -> reference
+ * SPSC ring -> reference worker_t -> GPU loop, optionally with a rule reload in the middle,
+ * for tests/test_gpu_dropin.py to compare with the reference worker; upe_dropin_bench() is the
+ * reference's own throughput benchmark (tests/benchmark_throughput.c: synthetic NIC producer ->
+ * rings -> workers -> stubbed TX, consumer Mpps = pkts_in / producer time) run with reference
+ * worker threads or with GPU workers, for bench.py.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <pthread.h>
+#include <sched.h>
 #include <signal.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "arp_table.h"
 #include "ndp_table.h"
@@ -39,85 +44,67 @@
 
 volatile sig_atomic_t g_stop = 0; /* defined by the program, reference src/main.c:27 */
 
-/* TX stubs, as reference tests/benchmark_throughput.c:30-42 */
+/* ---- TX stubs (as reference tests/benchmark_throughput.c:30-42), with a call log ---------- */
+/* The log (tests): per tx_send_batch call its size and each frame's pktbuf; tx_send frames. */
+static pktbuf_t **g_log_frames, **g_log_replies;
+static uint32_t *g_log_sizes;
+static size_t g_log_nf, g_log_nb, g_log_nr, g_log_cap;
+
+static pktbuf_t *buf_of(const uint8_t *data) {
+    return (pktbuf_t *)(data - offsetof(pktbuf_t, data));
+}
 int tx_send(const tx_ctx_t *ctx, const uint8_t *frame, size_t len) {
-    (void)ctx; (void)frame; (void)len;
+    (void)ctx; (void)len;
+    if (g_log_replies && g_log_nr < g_log_cap) g_log_replies[g_log_nr++] = buf_of(frame);
     return 0;
 }
 int tx_send_batch(const tx_ctx_t *ctx, const uint8_t *const *frames, const size_t *lens, int count) {
-    (void)ctx; (void)frames; (void)lens;
+    (void)ctx; (void)lens;
+    if (g_log_frames && g_log_nb < g_log_cap && g_log_nf + (size_t)count <= g_log_cap) {
+        g_log_sizes[g_log_nb++] = (uint32_t)count;
+        for (int i = 0; i < count; i++) g_log_frames[g_log_nf++] = buf_of(frames[i]);
+    }
     return count;
 }
 
-#define GPU_BATCH 65536u
-#define WIN UPE_HDR_WINDOW
-
+/* =========================================================================================== */
+/* The binding: upe_gpu_worker_run over a reference worker_t                                    */
+/* =========================================================================================== */
 typedef struct {
     worker_t *w;
     int device;
+    const upe_worker_ops_t *ops;    /* NULL: g_ops */
+    upe_worker_cfg_t cfg;
+    const rule_table_t *rt_loaded;  /* the table the context holds */
+    uint64_t stats_every_ns;        /* rule_stats published at most this often (0: every batch) */
+    uint64_t stats_last_ns;
+    upe_counters_t counters;        /* the loop's, at the end */
+    uint64_t consumed;              /* published: NS / NA consumed (no worker_t field) */
     int rc;
-    uint8_t *pool_base; /* mapped mode: the registered pktbuf array (frames classified in place) */
-} gpu_arg_t;
+} gpu_worker_t;
 
-/* 0: header windows through upe_gpu_process_host (copies); 1: the pktbufs classified where they
- * lie in the registered pool (upe_gpu_process_mapped, nothing copied). */
-static int g_mapped = 0;
-void upe_dropin_set_mapped(int mapped) { g_mapped = mapped; }
-
-/* The TX flush of the reference worker loop, src/worker.c:286-303. */
-static void flush_tx(worker_t *w) {
-    if (w->tx_count > 0) {
-        int sent = tx_send_batch(w->tx, w->tx_frames, w->tx_lens, w->tx_count);
-        if (sent < 0) sent = 0;
-        w->pkts_forwarded += (uint64_t)sent;
-        w->pkts_dropped += (uint64_t)(w->tx_count - sent);
-        for (int i = 0; i < w->tx_count; i++) pktbuf_free(w->pool, w->tx_bufs[i]);
-        w->tx_count = 0;
-    }
+static uint64_t now_ns(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-/* Byte k of a frame as a zero-filled pktbuf holds it (the reference reads the ethertype and the
- * ARP header without a length check, src/worker.c:24-35). */
-static uint8_t at(const pktbuf_t *b, size_t k) { return k < b->len ? b->data[k] : 0; }
-
-/* A packet handle_control_packet may write a neighbour table for (src/worker.c:28-39, 57-100):
- * ARP with the Ethernet/IPv4 header shape, or an IPv6 NS/NA of at least 78 bytes.  The batch is
- * cut after it, so every later packet sees the table write, as in the reference's burst loop. */
-static int is_table_write(const pktbuf_t *b) {
-    const unsigned et = (unsigned)at(b, 12) << 8 | at(b, 13);
-    if (et == 0x0806)
-        return at(b, 14) == 0 && at(b, 15) == 1 && at(b, 16) == 8 && at(b, 17) == 0 &&
-               at(b, 18) == 6 && at(b, 19) == 4;
-    return et == 0x86DD && b->len >= 78 && at(b, 20) == 58 && (at(b, 54) == 135 || at(b, 54) == 136);
+#define GW(u) ((gpu_worker_t *)(u))
+static unsigned op_pop(void *u, void **b, unsigned m) { return ring_pop_burst(GW(u)->w->rx_ring, b, m); }
+static int op_stop(void *u) { (void)u; return g_stop != 0; }
+static uint8_t *op_data(void *u, void *b) { (void)u; return ((pktbuf_t *)b)->data; }
+static size_t op_len(void *u, void *b) { (void)u; return ((pktbuf_t *)b)->len; }
+static void op_free(void *u, void *b) { pktbuf_free(GW(u)->w->pool, (pktbuf_t *)b); }
+static int op_tx_send(void *u, const uint8_t *f, size_t len) { return tx_send(GW(u)->w->tx, f, len); }
+static int op_tx_send_batch(void *u, const uint8_t *const *f, const size_t *lens, int count) {
+    return tx_send_batch(GW(u)->w->tx, f, lens, count);
 }
-
-/* handle_control_packet's table writes and ARP reply (src/worker.c:30-52, 64-95) for a packet the
- * GPU classified: v is its verdict, b->data the frame as the GPU left it (an answered ARP request
- * already rewritten into the reply, whose tha / tpa now hold the request's sha / spa). */
-static void control_writes(worker_t *w, pktbuf_t *b, uint32_t v) {
-    const uint8_t *d = b->data;
-    if (v & UPE_VF_ARP_LEARN) {
-        const int replied = (v & UPE_VF_ARP_REPLY) != 0;
-        uint32_t spa_be;
-        memcpy(&spa_be, d + (replied ? 38 : 28), 4);
-        arp_update(w->arpt, ntohl(spa_be), d + (replied ? 32 : 22));
-        if (replied) tx_send(w->tx, b->data, b->len);
-    } else if (UPE_VERDICT_CODE(v) == UPE_V_CONSUMED) {
-        const int ns = d[54] == 135;
-        for (size_t off = 78; off + 2 <= b->len;) {
-            const uint8_t type = d[off];
-            const size_t olen = (uint8_t)(d[off + 1] * 8); /* uint8_t, src/worker.c:73 */
-            if (olen == 0 || off + olen > b->len) break;
-            if (olen >= 8 && ((ns && type == 1) || (!ns && type == 2))) {
-                ndp_update(w->ndpt, ns ? d + 22 : d + 62, d + off + 2);
-                break;
-            }
-            off += olen;
-        }
-    }
+static void op_arp_update(void *u, uint32_t ip, const uint8_t mac[6]) { arp_update(GW(u)->w->arpt, ip, mac); }
+static void op_ndp_update(void *u, const uint8_t ip[16], const uint8_t mac[6]) {
+    ndp_update(GW(u)->w->ndpt, ip, mac);
 }
-
-static int load_tables(upe_gpu_ctx_t *ctx, worker_t *w) {
+static int op_load_neigh(void *u, upe_gpu_ctx_t *ctx) {
+    worker_t *w = GW(u)->w;
     pthread_rwlock_rdlock(&w->arpt->lock);
     pthread_rwlock_rdlock(&w->ndpt->lock);
     int rc = upe_gpu_load_neigh(ctx, (const upe_arp_entry_t *)w->arpt->entries, w->arpt->capacity,
@@ -126,130 +113,140 @@ static int load_tables(upe_gpu_ctx_t *ctx, worker_t *w) {
     pthread_rwlock_unlock(&w->arpt->lock);
     return rc;
 }
-
-typedef struct {
-    upe_gpu_ctx_t *ctx;
-    uint8_t *win;
-    uint64_t *desc;
-    uint32_t *verdict;
-    pktbuf_t **bufs;
-    size_t n;
-    uint8_t *pool_base; /* mapped mode */
-} gpu_batch_t;
-
-/* One GPU batch through the host round trip, then the reference's per-verdict handling
- * (src/worker.c:146-153 drops, :240-243 TX queue, :96-98 consumed) and, when the batch ends with
- * a table-writing control packet, that packet's writes and the new table snapshot. */
-static int run_batch(worker_t *w, gpu_batch_t *g, int cut) {
-    if (g->n == 0) return 0;
-    if (g->pool_base) {
-        /* the frames rewritten in place in the pool, where tx_send reads them */
-        if (upe_gpu_process_mapped(g->ctx, g->pool_base, g->desc, g->verdict, g->n, NULL) != 0 ||
-            upe_gpu_sync(g->ctx, NULL) != 0) {
-            fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
-            return -1;
-        }
-    } else if (upe_gpu_process_host(g->ctx, g->win, g->n * WIN + UPE_FRAME_TAIL, g->desc,
-                                    g->verdict, g->n, 0) != 0) {
-        fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
-        return -1;
+/* the stats thread swapped w->rt (and w->rule_stats) since the context's table was loaded */
+static int op_poll(void *u) { return GW(u)->w->rt != GW(u)->rt_loaded; }
+static int op_sync(void *u, upe_gpu_ctx_t *ctx) {
+    const rule_table_t *rt = GW(u)->w->rt;
+    GW(u)->rt_loaded = rt;
+    /* old rule_stats are not handed back: the stats thread frees the old array */
+    return upe_gpu_reload_rules(ctx, (const upe_rule_t *)rt->rules, rt->count, rt->capacity, NULL, 0);
+}
+static void op_publish(void *u, upe_gpu_ctx_t *ctx, const upe_counters_t *c) {
+    gpu_worker_t *g = GW(u);
+    worker_t *w = g->w;
+    /* rule_stats into the array the stats thread reads — unless a swap is pending: the packets
+     * just classified ran with the old table, and w->rule_stats is already the new array */
+    const uint64_t t = now_ns();
+    if (w->rt == g->rt_loaded && t - g->stats_last_ns >= g->stats_every_ns) {
+        g->stats_last_ns = t;
+        (void)upe_gpu_get_stats(ctx, NULL, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity);
     }
-    for (size_t i = 0; i < g->n; i++) {
-        pktbuf_t *b = g->bufs[i];
-        const uint32_t v = g->verdict[i];
-        if (!g->pool_base)
-            memcpy(b->data, g->win + i * WIN, b->len < UPE_REWRITE_EXTENT ? b->len : UPE_REWRITE_EXTENT);
-        if (cut && i + 1 == g->n) control_writes(w, b, v);
-        if (UPE_VERDICT_CODE(v) == UPE_V_FWD) {
-            w->tx_frames[w->tx_count] = b->data; /* worker.c:240-243 */
-            w->tx_lens[w->tx_count] = b->len;
-            w->tx_bufs[w->tx_count++] = b;
-            if (w->tx_count == WORKER_BURST_SIZE) flush_tx(w);
-        } else if (UPE_VERDICT_CODE(v) == UPE_V_CONSUMED) {
-            pktbuf_free(w->pool, b); /* consumed control packet: no counter */
-        } else {
-            w->pkts_dropped++; /* every drop path of process_packet counts one */
-            pktbuf_free(w->pool, b);
-        }
-    }
-    flush_tx(w);
-    g->n = 0;
-    return cut ? load_tables(g->ctx, w) : 0;
+    /* then the counters (release: a reader that sees them sees the rule_stats above) */
+    __atomic_store_n(&w->pkts_in, c->pkts_in, __ATOMIC_RELEASE);
+    __atomic_store_n(&w->pkts_parsed, c->pkts_parsed, __ATOMIC_RELEASE);
+    __atomic_store_n(&w->pkts_matched, c->pkts_matched, __ATOMIC_RELEASE);
+    __atomic_store_n(&w->pkts_forwarded, c->pkts_forwarded, __ATOMIC_RELEASE);
+    __atomic_store_n(&g->consumed, c->pkts_consumed, __ATOMIC_RELEASE);
+    __atomic_store_n(&w->pkts_dropped, c->pkts_dropped, __ATOMIC_RELEASE);
 }
 
-/* GPU-backed replacement of worker_main (reference src/worker.c:255-307). */
+static const upe_worker_ops_t g_ops = {
+    op_pop, op_stop, op_data, op_len, op_free, op_tx_send, op_tx_send_batch,
+    op_arp_update, op_ndp_update, op_load_neigh, op_poll, op_sync, op_publish,
+};
+
+/* The GPU worker thread: what worker_main is for a CPU worker. */
 static void *gpu_worker_main(void *arg) {
-    gpu_arg_t *ga = arg;
-    worker_t *w = ga->w;
-    ga->rc = -1;
-    gpu_batch_t g;
-    memset(&g, 0, sizeof g);
-    g.ctx = upe_gpu_open(ga->device, w->rt->capacity);
-    g.win = upe_gpu_host_alloc((size_t)GPU_BATCH * WIN + UPE_FRAME_TAIL);
-    g.desc = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint64_t));
-    g.verdict = upe_gpu_host_alloc(GPU_BATCH * sizeof(uint32_t));
-    g.bufs = malloc(GPU_BATCH * sizeof(*g.bufs));
-    g.pool_base = ga->pool_base;
-    if (!g.ctx || !g.win || !g.desc || !g.verdict || !g.bufs) return NULL;
-    if (upe_gpu_load_rules(g.ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
-        load_tables(g.ctx, w) != 0 || upe_gpu_set_port(g.ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0)
-        return NULL;
-    void *burst[WORKER_BURST_SIZE];
-    for (;;) {
-        unsigned k = ring_pop_burst(w->rx_ring, burst, WORKER_BURST_SIZE); /* worker.c:268 */
-        w->pkts_in += k;                                                   /* worker.c:280 */
-        for (unsigned j = 0; j < k; j++) {
-            pktbuf_t *b = burst[j];
-            if (g.pool_base) {
-                /* the pktbuf's data where it lies: offset into the registered pool */
-                g.desc[g.n] = UPE_DESC((uint64_t)(b->data - g.pool_base), b->len);
-            } else {
-                size_t c = b->len < WIN ? b->len : WIN;
-                memcpy(g.win + g.n * WIN, b->data, c);
-                memset(g.win + g.n * WIN + c, 0, WIN - c);
-                g.desc[g.n] = UPE_DESC((uint64_t)g.n * WIN, b->len);
-            }
-            g.bufs[g.n++] = b;
-            const int cut = is_table_write(b);
-            if ((cut || g.n == GPU_BATCH) && run_batch(w, &g, cut) != 0) return NULL;
-        }
-        const int stop = k == 0 && g_stop;
-        if (k == 0 && g.n > 0 && run_batch(w, &g, 0) != 0) return NULL;
-        if (stop) break;
+    gpu_worker_t *g = arg;
+    worker_t *w = g->w;
+    g->rc = -1;
+    if (w->core_id >= 0) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(w->core_id, &one);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
     }
-    /* the counters the GPU keeps, into the reference's own worker_t fields */
-    upe_counters_t c;
-    if (upe_gpu_get_stats(g.ctx, &c, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity) != 0)
+    upe_gpu_ctx_t *ctx = upe_gpu_open(g->device, w->rt->capacity);
+    if (!ctx) {
+        fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
         return NULL;
-    w->pkts_parsed = c.pkts_parsed;
-    w->pkts_matched = c.pkts_matched;
-    upe_gpu_host_free(g.win);
-    upe_gpu_host_free(g.desc);
-    upe_gpu_host_free(g.verdict);
-    free(g.bufs);
-    upe_gpu_close(g.ctx);
-    ga->rc = 0;
+    }
+    g->rt_loaded = w->rt;
+    if (upe_gpu_load_rules(ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
+        op_load_neigh(g, ctx) != 0 || upe_gpu_set_port(ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0 ||
+        upe_gpu_worker_run(ctx, g->ops ? g->ops : &g_ops, g, &g->cfg, &g->counters) != 0) {
+        fprintf(stderr, "dropin: %s\n", upe_gpu_last_error());
+        upe_gpu_close(ctx);
+        return NULL;
+    }
+    g->stats_every_ns = 0;
+    op_publish(g, ctx, &g->counters); /* the final counters and rule_stats */
+    upe_gpu_close(ctx);
+    g->rc = 0;
     return NULL;
+}
+
+/* worker_start() for a GPU worker (reference src/worker.c:336-339). */
+static int gpu_worker_start(gpu_worker_t *g, pthread_t *th) {
+    return pthread_create(th, NULL, gpu_worker_main, g);
+}
+
+/* =========================================================================================== */
+/* Tests: a stream through the reference pipeline with the GPU worker                           */
+/* =========================================================================================== */
+static int g_mapped = 0;
+void upe_dropin_set_mapped(int mapped) { g_mapped = mapped; }
+
+/* Burst sizes the worker popped (tests): wraps ring_pop_burst. */
+static uint32_t *g_log_pops;
+static size_t g_log_np;
+static unsigned op_pop_logged(void *u, void **b, unsigned m) {
+    unsigned k = op_pop(u, b, m);
+    if (k && g_log_pops && g_log_np < g_log_cap) g_log_pops[g_log_np++] = k;
+    return k;
+}
+
+static size_t index_of(pktbuf_t *const *all, size_t n, const pktbuf_t *b) {
+    /* `all` holds the run's buffers in packet order; they are distinct pool slots */
+    static const pktbuf_t *const *s_all;
+    static size_t s_n, *s_idx, s_lo, s_span;
+    if (s_all != (const pktbuf_t *const *)all || s_n != n) {
+        s_all = (const pktbuf_t *const *)all;
+        s_n = n;
+        size_t lo = (size_t)-1, hi = 0;
+        for (size_t i = 0; i < n; i++) {
+            size_t a = (size_t)all[i];
+            lo = a < lo ? a : lo;
+            hi = a > hi ? a : hi;
+        }
+        s_lo = lo;
+        s_span = (hi - lo) / sizeof(pktbuf_t) + 1;
+        free(s_idx);
+        s_idx = malloc(s_span * sizeof(size_t));
+        for (size_t i = 0; i < n; i++) s_idx[((size_t)all[i] - lo) / sizeof(pktbuf_t)] = i;
+    }
+    return s_idx[((size_t)b - s_lo) / sizeof(pktbuf_t)];
 }
 
 /*
  * Run `n` packets (batch layout of include/upe_gpu.h) through: an RX-like producer thread ->
- * reference SPSC ring -> reference worker_t driven by gpu_worker_main.  rules in insertion order
- * (rule_table_add), neighbour slot arrays copied into reference tables.  Outputs the worker's
- * counters (pkts_in, parsed, matched, forwarded, dropped), rule_stats[capacity], each packet's
- * bytes as the worker left them in its pktbuf (out_frames, the input's layout) and the final
- * neighbour slot arrays (out_arp / out_ndp, the input capacities).
+ * reference SPSC ring -> reference worker_t driven by the GPU worker loop.  rules in insertion
+ * order (rule_table_add), neighbour slot arrays copied into reference tables.  Outputs the
+ * worker's counters (pkts_in, parsed, matched, forwarded, dropped), rule_stats[capacity], each
+ * packet's bytes as the worker left them in its pktbuf (out_frames, the input's layout), the
+ * final neighbour slot arrays (out_arp / out_ndp, the input capacities), and the TX / ring log
+ * (optional, `log_cap` entries each): pops[] = burst sizes popped, sizes[] = tx_send_batch call
+ * sizes, tx[] = packet index of each frame sent, replies[] = packet index of each tx_send;
+ * log_n[4] = their lengths.
+ * Reload (rules_b != NULL): after the first `at` packets have been processed, the driver does
+ * what the stats thread does on SIGHUP (src/main.c:237-265: new table of capacity cap_b from
+ * rules_b in insertion order, fresh calloc'd rule_stats, both swapped into the worker_t) and
+ * pushes the rest; stats_a receives the old rule_stats array as it was at the swap, and
+ * rule_stats the new one (cap_b entries).
  */
 int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
                    const upe_arp_entry_t *arp, size_t arp_cap, const upe_ndp_entry_t *ndp,
                    size_t ndp_cap, const uint8_t eth_addr[6], uint32_t ip4_addr,
                    const uint8_t *frames, const uint64_t *in_desc, size_t n, int device,
                    uint64_t counters[5], upe_rule_stat_t *rule_stats, uint8_t *out_frames,
-                   upe_arp_entry_t *out_arp, upe_ndp_entry_t *out_ndp) {
-    rule_table_t rt;
-    if (rule_table_init(&rt, capacity) != 0) return -1;
+                   upe_arp_entry_t *out_arp, upe_ndp_entry_t *out_ndp,
+                   const upe_rule_t *rules_b, size_t nrules_b, size_t cap_b, size_t at,
+                   upe_rule_stat_t *stats_a, size_t log_cap, uint32_t *pops, uint32_t *sizes,
+                   uint32_t *tx, uint32_t *replies, uint64_t log_n[4]) {
+    rule_table_t *rt = malloc(sizeof *rt);
+    if (!rt || rule_table_init(rt, capacity) != 0) return -1;
     for (size_t i = 0; i < nrules; i++)
-        if (rule_table_add(&rt, (const rule_t *)&rules[i]) != 0) return -1;
+        if (rule_table_add(rt, (const rule_t *)&rules[i]) != 0) return -1;
     arp_table_t arpt;
     ndp_table_t ndpt;
     if (arp_table_init(&arpt, arp_cap ? arp_cap : 1) != 0 ||
@@ -257,10 +254,10 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
         return -1;
     if (arp_cap) memcpy(arpt.entries, arp, arp_cap * sizeof(arp_entry_t));
     if (ndp_cap) memcpy(ndpt.entries, ndp, ndp_cap * sizeof(ndp_entry_t));
-    tx_ctx_t tx;
-    memset(&tx, 0, sizeof tx);
-    memcpy(tx.eth_addr, eth_addr, 6);
-    tx.ip4_addr = ip4_addr;
+    tx_ctx_t txc;
+    memset(&txc, 0, sizeof txc);
+    memcpy(txc.eth_addr, eth_addr, 6);
+    txc.ip4_addr = ip4_addr;
     /* One pool per process (the pool's thread-local caches remember it), sized so that every
      * packet of the run gets its own buffer: the producer allocates all of them before the
      * worker frees any, so the test does not lean on concurrent alloc/free in the pool. */
@@ -269,9 +266,10 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     /* (slack: every finished worker thread takes up to LOCAL_CACHE_SIZE buffers with it in its
      * thread-local cache, reference src/pktbuf.c:10) */
     if (pool_cap < n + 256) {
-        if (pool_cap) return -1; /* one size per process */
-        if (pktbuf_pool_init(&pool, n + 8192) != 0) return -1;
-        pool_cap = n + 8192;
+        if (pool_cap) return -1; /* one size per process: room for the largest test stream */
+        const size_t want = n + 8192 > ((size_t)1 << 19) ? n + 8192 : (size_t)1 << 19;
+        if (pktbuf_pool_init(&pool, want) != 0) return -1;
+        pool_cap = want;
     }
     /* mapped mode: the pool's buffers page-locked and mapped for the GPU once */
     static int pool_registered;
@@ -294,16 +292,67 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     spsc_ring_t ring;
     if (ring_init(&ring, 1024) != 0) return -1;
     worker_t *w = calloc(1, sizeof(worker_t)); /* src/main.c:444 */
-    if (!w || worker_init(w, 0, -1, &ring, &pool, &rt, &tx, &arpt, &ndpt) != 0) return -1;
+    if (!w || worker_init(w, 0, -1, &ring, &pool, rt, &txc, &arpt, &ndpt) != 0) return -1;
+
+    /* the TX / ring log */
+    g_log_cap = log_cap;
+    g_log_nb = g_log_nf = g_log_nr = g_log_np = 0;
+    pktbuf_t **lf = log_cap ? malloc(log_cap * sizeof(*lf)) : NULL;
+    pktbuf_t **lr = log_cap ? malloc(log_cap * sizeof(*lr)) : NULL;
+    g_log_frames = lf;
+    g_log_replies = lr;
+    g_log_sizes = log_cap ? sizes : NULL;
+    g_log_pops = log_cap ? pops : NULL;
 
     g_stop = 0;
-    gpu_arg_t ga = {w, device, -1, g_mapped ? (uint8_t *)pool.buffers : NULL};
+    gpu_worker_t g;
+    memset(&g, 0, sizeof g);
+    g.w = w;
+    g.device = device;
+    g.cfg.pool_base = g_mapped ? (uint8_t *)pool.buffers : NULL;
+    g.cfg.batch = 65536;
+    /* (rule_stats published after every batch, so that the array swapped out at a reload holds
+     * exactly the counts up to the swap) */
+    static upe_worker_ops_t ops;
+    ops = g_ops;
+    ops.pop_burst = op_pop_logged;
+    g.ops = &ops;
     pthread_t th;
-    pthread_create(&th, NULL, gpu_worker_main, &ga);
+    if (gpu_worker_start(&g, &th) != 0) return -1;
     /* producer: the RX thread's staged bursts of 32 into the ring, src/rx_pcap.c:80-92 */
-    for (size_t i = 0; i < n; i += 32) {
-        unsigned ns = (unsigned)(n - i < 32 ? n - i : 32), done = 0;
+    rule_stat_t *old_stats = NULL;
+    rule_table_t *rt_b = NULL;
+    const size_t first = rules_b && at < n ? at : n;
+    for (size_t i = 0; i < first; i += 32) {
+        unsigned ns = (unsigned)(first - i < 32 ? first - i : 32), done = 0;
         while (done < ns) done += ring_push_burst(&ring, (void **)(all + i) + done, ns - done);
+    }
+    if (rules_b) {
+        /* wait until the first part is processed: every packet forwarded, dropped or consumed
+         * (the counters the loop publishes after each batch) */
+        for (;;) {
+            const uint64_t done = __atomic_load_n(&w->pkts_dropped, __ATOMIC_ACQUIRE) +
+                                  __atomic_load_n(&w->pkts_forwarded, __ATOMIC_ACQUIRE) +
+                                  __atomic_load_n(&g.consumed, __ATOMIC_ACQUIRE);
+            if (done >= first) break;
+            struct timespec ts = {0, 100000};
+            nanosleep(&ts, NULL);
+        }
+        /* the stats thread's reload, src/main.c:222-265 */
+        rt_b = malloc(sizeof *rt_b);
+        if (!rt_b || rule_table_init(rt_b, cap_b) != 0) return -1;
+        for (size_t i = 0; i < nrules_b; i++)
+            if (rule_table_add(rt_b, (const rule_t *)&rules_b[i]) != 0) return -1;
+        rule_stat_t *new_stats = calloc(rt_b->capacity, sizeof(rule_stat_t));
+        if (!new_stats) return -1;
+        old_stats = w->rule_stats;
+        memcpy(stats_a, old_stats, capacity * sizeof(rule_stat_t));
+        __atomic_store_n(&w->rule_stats, new_stats, __ATOMIC_RELEASE);
+        __atomic_store_n(&w->rt, rt_b, __ATOMIC_RELEASE);
+        for (size_t i = first; i < n; i += 32) {
+            unsigned ns = (unsigned)(n - i < 32 ? n - i : 32), done = 0;
+            while (done < ns) done += ring_push_burst(&ring, (void **)(all + i) + done, ns - done);
+        }
     }
     g_stop = 1;
     pthread_join(th, NULL);
@@ -312,18 +361,216 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     counters[2] = w->pkts_matched;
     counters[3] = w->pkts_forwarded;
     counters[4] = w->pkts_dropped;
-    if (rule_stats) memcpy(rule_stats, w->rule_stats, capacity * sizeof(rule_stat_t));
+    if (rule_stats) memcpy(rule_stats, w->rule_stats, w->rt->capacity * sizeof(rule_stat_t));
     if (out_frames)
         for (size_t i = 0; i < n; i++)
             memcpy(out_frames + (size_t)(in_desc[i] >> 16), all[i]->data, (size_t)(in_desc[i] & 0xFFFF));
     if (out_arp && arp_cap) memcpy(out_arp, arpt.entries, arp_cap * sizeof(arp_entry_t));
     if (out_ndp && ndp_cap) memcpy(out_ndp, ndpt.entries, ndp_cap * sizeof(ndp_entry_t));
+    if (log_cap) {
+        for (size_t k = 0; k < g_log_nf; k++) tx[k] = (uint32_t)index_of(all, n, lf[k]);
+        for (size_t k = 0; k < g_log_nr; k++) replies[k] = (uint32_t)index_of(all, n, lr[k]);
+        log_n[0] = g_log_np;
+        log_n[1] = g_log_nb;
+        log_n[2] = g_log_nf;
+        log_n[3] = g_log_nr;
+    }
+    g_log_frames = g_log_replies = NULL;
+    g_log_sizes = g_log_pops = NULL;
+    free(lf);
+    free(lr);
     worker_destroy(w);
     free(w);
+    free(old_stats);
     free(all);
     ring_destroy(&ring);
     arp_table_destroy(&arpt);
     ndp_table_destroy(&ndpt);
+    rule_table_destroy(rt);
+    free(rt);
+    if (rt_b) {
+        rule_table_destroy(rt_b);
+        free(rt_b);
+    }
+    return g.rc;
+}
+
+/* =========================================================================================== */
+/* The reference's throughput benchmark with CPU or GPU workers                                 */
+/* =========================================================================================== */
+/* build_dummy_packet of reference tests/benchmark_throughput.c:138-175: Eth + IPv4 (TTL 64,
+ * 10.128.0.1 -> 10.128.0.2) + TCP 45000 -> 80, zero padded to packet_size. */
+static void build_dummy_packet(pktbuf_t *b, int packet_size) {
+    b->len = (size_t)packet_size;
+    uint8_t *p = b->data;
+    memset(p, 0, (size_t)packet_size);
+    p[12] = 0x08;
+    p[13] = 0x00;
+    p += 14;
+    p[0] = 0x45;
+    p[2] = (uint8_t)((packet_size - 14) >> 8);
+    p[3] = (uint8_t)((packet_size - 14) & 0xFF);
+    p[8] = 64;
+    p[9] = 6;
+    p[12] = 10; p[13] = 128; p[14] = 0; p[15] = 1;
+    p[16] = 10; p[17] = 128; p[18] = 0; p[19] = 2;
+    p += 20;
+    p[0] = 0xAF; p[1] = 0xC8;
+    p[2] = 0x00; p[3] = 0x50;
+    p[12] = 0x50;
+}
+
+static double mono_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC_RAW, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* run_producer of reference tests/benchmark_throughput.c:188-238: allocate, build, push round
+ * robin over the workers' rings, free what a full ring refuses; returns pushes, full events. */
+static void producer(pktbuf_pool_t *pool, spsc_ring_t *rings, int nw, int batch, int psize,
+                     double seconds, uint64_t *pushed, uint64_t *full, double *dur) {
+    void *b[256];
+    int ring_idx = 0, check = 0;
+    *pushed = *full = 0;
+    const double start = mono_s(), deadline = start + seconds;
+    double now = start;
+    while (now < deadline) {
+        int actual = 0;
+        for (int i = 0; i < batch; i++) {
+            pktbuf_t *p = pktbuf_alloc(pool);
+            if (!p) break;
+            build_dummy_packet(p, psize);
+            b[actual++] = p;
+        }
+        if (actual == 0) {
+            struct timespec ts = {0, 1000};
+            nanosleep(&ts, NULL);
+            now = mono_s();
+            check = 0;
+            continue;
+        }
+        unsigned pu = ring_push_burst(&rings[ring_idx], b, (unsigned)actual);
+        *pushed += pu;
+        if (pu < (unsigned)actual) {
+            (*full)++;
+            for (unsigned i = pu; i < (unsigned)actual; i++) pktbuf_free(pool, b[i]);
+        }
+        ring_idx = (ring_idx + 1) % nw;
+        if (++check >= 128) {
+            now = mono_s();
+            check = 0;
+        }
+    }
+    *dur = mono_s() - start;
+}
+
+/*
+ * The reference benchmark's setup (tests/benchmark_throughput.c:87-116: one TCP FWD rule, one ARP
+ * entry for 10.128.0.2, tx MAC ..:bb) with `workers` workers: gpu = 0 the reference's own
+ * worker threads (worker_start -> src/worker.c worker_main), gpu = 1 GPU workers (one context
+ * each on `device`, gpu_worker_start -> upe_gpu_worker_run; mapped = 1 classifies the pool's
+ * pktbufs where they lie, else header windows through the DMA round trip).  The calling thread
+ * is the producer, pinned to cpus[0]; worker t is pinned to cpus[1 + t] (cpus may be NULL).
+ * warmup then `seconds` of measurement.  out[0] = consumer Mpps (pkts_in delta over the
+ * producer's time, as output_json reports it), out[1] = producer Mpps, out[2] = ring-full
+ * events, out[3] = seconds, out[4] = packets consumed.  0 / -1.
+ */
+int upe_dropin_bench(int gpu, int mapped, int workers, int device, size_t pool_cap,
+                     size_t ring_size, int batch, int packet_size, double warmup, double seconds,
+                     size_t gpu_batch, const int *cpus, double out[5]) {
+    if (workers < 1 || workers > 16 || batch < 1 || batch > 256) return -1;
+    if (cpus) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[0], &one);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+    }
+    /* one pool per capacity, kept for the process's life: a thread's pktbuf cache remembers
+     * its pool (src/pktbuf.c:298-303) and flushes into it when the thread switches pools */
+    static pktbuf_pool_t pools[4];
+    static size_t caps[4];
+    static int registered[4];
+    int pi = 0;
+    while (pi < 4 && caps[pi] && caps[pi] != pool_cap) pi++;
+    if (pi == 4) return -1;
+    if (!caps[pi]) {
+        if (pktbuf_pool_init(&pools[pi], pool_cap) != 0) return -1;
+        caps[pi] = pool_cap;
+    }
+    pktbuf_pool_t *const poolp = &pools[pi];
+#define pool (*poolp)
+    if (gpu && mapped && !registered[pi]) {
+        if (upe_gpu_host_register(pool.buffers, pool.capacity * sizeof(pktbuf_t)) != 0) return -1;
+        registered[pi] = 1;
+    }
+    spsc_ring_t *rings = calloc((size_t)workers, sizeof(spsc_ring_t));
+    for (int i = 0; i < workers; i++)
+        if (ring_init(&rings[i], ring_size) != 0) return -1;
+    rule_table_t rt;
+    rule_table_init(&rt, 1024);
+    rule_t r = {.priority = 10, .protocol = 6, .action = {.type = ACT_FWD, .out_ifindex = 1}};
+    rule_table_add(&rt, &r);
+    arp_table_t arpt;
+    ndp_table_t ndpt;
+    arp_table_init(&arpt, 1024);
+    const uint32_t dst_ip = (10U << 24) | (128U << 16) | (0U << 8) | 2U;
+    const uint8_t dst_mac[6] = {0xaa, 0x00, 0x00, 0x00, 0x00, 0xbb};
+    arp_update(&arpt, dst_ip, dst_mac);
+    ndp_table_init(&ndpt, 1024);
+    tx_ctx_t txc;
+    memset(&txc, 0, sizeof txc);
+    txc.eth_addr[5] = 0xbb;
+    worker_t *ws = calloc((size_t)workers, sizeof(worker_t));
+    gpu_worker_t *gs = calloc((size_t)workers, sizeof(gpu_worker_t));
+    pthread_t *th = calloc((size_t)workers, sizeof(pthread_t));
+    g_stop = 0;
+    for (int i = 0; i < workers; i++) {
+        worker_init(&ws[i], i, cpus ? cpus[1 + i] : -1, &rings[i], &pool, &rt, &txc, &arpt, &ndpt);
+        if (gpu) {
+            gs[i].w = &ws[i];
+            gs[i].device = device;
+            gs[i].cfg.pool_base = mapped ? (uint8_t *)pool.buffers : NULL;
+            gs[i].cfg.batch = gpu_batch;
+            gs[i].stats_every_ns = 100000000ull; /* rule_stats for the stats thread: 10 Hz */
+            if (gpu_worker_start(&gs[i], &th[i]) != 0) return -1;
+        } else if (worker_start(&ws[i]) != 0) {
+            return -1;
+        }
+    }
+    uint64_t pushed, full;
+    double dur;
+    if (warmup > 0) producer(&pool, rings, workers, batch, packet_size, warmup, &pushed, &full, &dur);
+    uint64_t before[16];
+    for (int i = 0; i < workers; i++) before[i] = __atomic_load_n(&ws[i].pkts_in, __ATOMIC_ACQUIRE);
+    producer(&pool, rings, workers, batch, packet_size, seconds, &pushed, &full, &dur);
+    uint64_t consumed = 0;
+    for (int i = 0; i < workers; i++)
+        consumed += __atomic_load_n(&ws[i].pkts_in, __ATOMIC_ACQUIRE) - before[i];
+    g_stop = 1;
+    int rc = 0;
+    for (int i = 0; i < workers; i++) {
+        if (gpu) {
+            pthread_join(th[i], NULL);
+            rc |= gs[i].rc;
+        } else {
+            worker_join(&ws[i]);
+        }
+    }
+    out[0] = (double)consumed / dur / 1e6;
+    out[1] = (double)pushed / dur / 1e6;
+    out[2] = (double)full;
+    out[3] = dur;
+    out[4] = (double)consumed;
+    for (int i = 0; i < workers; i++) worker_destroy(&ws[i]);
+    for (int i = 0; i < workers; i++) ring_destroy(&rings[i]);
+    free(ws);
+    free(gs);
+    free(th);
+    free(rings);
     rule_table_destroy(&rt);
-    return ga.rc;
+    arp_table_destroy(&arpt);
+    ndp_table_destroy(&ndpt);
+    return rc;
+#undef pool
 }

@@ -110,3 +110,43 @@ def test_reload_rejects_bad_tables_and_keeps_the_old(gpu_worker_factory):
     _assert_same((frames, verdict, counters, stats, l1),
                  {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                   "rule_stats": r.rule_stats, "l1": r.l1}, "after refused reloads")
+
+
+@pytest.mark.parametrize("host", [False, True], ids=["device", "host-emit"])
+def test_reload_in_a_stream_of_batches(gpu_worker_factory, host):
+    """Many small batches before and after the reload (the kernel without look-back is in use by
+    then), device-resident or through the emit-mode host round trip."""
+    import dataclasses
+
+    wl, rules_b, at, cap_b = reload_util.case("B")
+    wl = dataclasses.replace(wl, desc=wl.desc[:40_000])
+    at = 20_480
+    ref, old_ref = oracle.run_reference_reload(wl, rules_b, cap_b, at)
+    w = gpu_worker_factory(wl.capacity)
+    verdict = np.zeros(wl.n, np.uint32)
+    frames = wl.frames.copy()
+    try:
+        w.configure(wl)
+        bounds = list(range(0, wl.n, 1024)) + [wl.n]
+        for s, e in zip(bounds[:-1], bounds[1:]):
+            if s == at:
+                old = w.reload_rules(ref.rules_sorted, cap_b)
+            if host:
+                rec = np.zeros((e - s, 16), np.uint8)
+                v = np.zeros(e - s, np.uint32)
+                w.process_host_emit(frames, wl.desc[s:e].copy(), v, rec, 0, 0)
+                verdict[s:e] = v
+            else:
+                b = gpu.DeviceBatch(w, frames, wl.desc[s:e])
+                b.run()
+                frames, verdict[s:e] = b.fetch()
+                b.free()
+        counters, stats = w.get_stats()
+        l1 = w.get_l1()
+    finally:
+        w.close()
+    assert np.array_equal(old, old_ref)
+    _assert_same((frames, verdict, counters, stats, l1),
+                 {"verdict": ref.verdict, "frames": ref.frames, "counters": ref.counters,
+                  "rule_stats": ref.rule_stats, "l1": ref.l1}, f"stream reload host={host}",
+                 batch_relative=True)

@@ -4,10 +4,10 @@
 set -e
 out=$(realpath -m "$1"); shift
 cd "$(dirname "$0")/.."
-make -s -C upe_amd/csrc "$PWD/build/upe_host.o" >/dev/null
+make -s -C upe_amd/csrc "$PWD/build/upe_host.o" "$PWD/build/upe_worker.o" >/dev/null
 tmp=$(mktemp -d)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" \
   -c -o $tmp/g.o upe_amd/csrc/upe_gpu.hip
 mkdir -p "$(dirname "$out")"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" $tmp/g.o build/upe_host.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" $tmp/g.o build/upe_host.o build/upe_worker.o
 rm -rf $tmp

@@ -7,7 +7,7 @@ set -e
 cfg=${1:-B}; shift || true
 mode=${1:-emit}; shift || true
 groups=${*:-fetch write sq clk}
-steps="--steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg --mode $mode --no-other-mode --no-imix"
+steps="--steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg --mode $mode --no-other-mode --no-imix --ring 0 --config-d-steps 0"
 for g in $groups; do
   case $g in
     fetch) ctr="FETCH_SIZE" ;;

@@ -126,8 +126,8 @@ constexpr int kRingMax = 64;           // batches of a ring launch whose complet
 #ifndef UPE_ABLATE
 #define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
 #endif
-// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 64 empty classify, 256 no fold of the
-// previous batch into the L1 state
+// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 16 general path, 64 empty classify,
+// 256 no fold of the previous batch into the L1 state
 constexpr unsigned kAblate = UPE_ABLATE;
 // Cache policy of the emit-mode record store: sc1 (buffer aux 16) writes the records through
 // and drops their lines from the XCD's L2, so the end of a launch has ~16 MB less dirty data to
@@ -818,7 +818,7 @@ struct Port {
     uint32_t mac_lo, mac_hi, ip4;
 };
 __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r,
-                                             const uint32_t (&win)[20]) {
+                                             const uint32_t (&win)[24]) {
     r.ok = false; r.consumed = false; r.v6 = false; r.flags = 0;
     r.proto = r.sport = r.dport = 0;
 #pragma unroll
@@ -827,9 +827,13 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
     // bytes 0..95 (IPv4 options reach 94): the window, and bytes 80..95 when the frame has them
     uint32_t w[24];
 #pragma unroll
-    for (int j = 0; j < 20; ++j) w[j] = win[j];
-    w[20] = w[21] = w[22] = w[23] = 0;
-    if (len > 80u) {
+    for (int j = 0; j < 24; ++j) w[j] = win[j];
+    // Bytes 80..95 matter only to an IPv4 TCP header behind 52 or more bytes of IPv4 header (its
+    // data-offset byte is byte 14 + 4 * IHL + 12): loaded here, for such frames only (loading
+    // them with every window instead measured no faster for config D, 713 vs 715 us per 16M,
+    // and slower for C in place, 57.3 vs 59.0 us: profiles/r04/v3_win6_ab.txt).
+    if (len > 80u && (w[3] & 0xFFFFu) == 0x0008u && (byte_of(w[3], 2) & 0xFu) >= 14u &&
+        byte_of(w[5], 3) == 6u) {
         const uint4 v = reinterpret_cast<const uint4*>(p)[5];
         w[20] = v.x; w[21] = v.y; w[22] = v.z; w[23] = v.w;
     }
@@ -1139,14 +1143,20 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
 
+    // The next chunk's window issued in the middle of the current chunk (after its rule match),
+    // so that its loads fly during the rest of it: into named registers carried into the next
+    // iteration (not an array the compiler might place in scratch).  Only the linear-scan
+    // kernels: the tuple-space ones have no registers to spare.
+    constexpr bool kMid = (UPE_MID_PREFETCH & 1) && (!kTssMode || (UPE_MID_PREFETCH & 4)) &&
+                          (kEmit || (UPE_MID_PREFETCH & 2));
     // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past len
     // are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame costs
     // four loads, not five.  Frames shorter than 49 bytes never take the fast path.
     // (A header-split batch, a.slab: bytes 0..63 as one dense 64-byte row per packet — whole
     // lines, coalesced across the wave — and bytes 64..79 from the frame when it has them.)
-    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[20], uint32_t pi) {
+    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[24], uint32_t pi) {
 #pragma unroll
-        for (int j = 0; j < 20; ++j) w[j] = 0;
+        for (int j = 0; j < 24; ++j) w[j] = 0;
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
@@ -1160,12 +1170,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
         }
     };
-    // The next chunk's window issued in the middle of the current chunk (after its rule match),
-    // so that its loads fly during the rest of it: into named registers carried into the next
-    // iteration (not an array the compiler might place in scratch).  Only the linear-scan
-    // kernels: the tuple-space ones have no registers to spare.
-    constexpr bool kMid = (UPE_MID_PREFETCH & 1) && (!kTssMode || (UPE_MID_PREFETCH & 4)) &&
-                          (kEmit || (UPE_MID_PREFETCH & 2));
     struct Win { uint4 c0, c1, c2, c3, c4; };
     auto fetch_window = [&](uint64_t dsc, bool live, uint32_t pi) -> Win {
         const uint4 z = make_uint4(0, 0, 0, 0);
@@ -1335,13 +1339,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // frames are 16-byte aligned: the offset in 16-byte units fits one register
         const uint32_t off16 = (uint32_t)(dsc >> 20);
         uint8_t* p = a.frames + ((size_t)off16 << 4);
-        uint32_t w[20];
+        uint32_t w[24];
         if (kMid && have_nw) {
             const uint4 c[5] = {nw.c0, nw.c1, nw.c2, nw.c3, nw.c4};
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 w[4 * j + 0] = c[j].x; w[4 * j + 1] = c[j].y; w[4 * j + 2] = c[j].z; w[4 * j + 3] = c[j].w;
             }
+            w[20] = w[21] = w[22] = w[23] = 0;
         } else {
             load_window(dsc, live, w, i);
         }
@@ -1396,7 +1401,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
 
         // ---- general path, for the waves that hold anything else ----
-        const bool slow = live && !fast4 && !fast6;
+        const bool slow = live && !fast4 && !fast6 && !(kAblate & 16);
         if (__any(slow) && slow) {
             Parsed g;
             general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g, w);
@@ -2167,7 +2172,8 @@ struct upe_gpu_ctx {
     uint32_t t_left = 0;           // calls left in the open sample (0: none open)
     uint64_t timing_launches = 0;  // calls covered by closed samples
     std::vector<hipEvent_t> ev;   // event pool, 2 per timed process() call
-    size_t ev_used = 0;
+    size_t ev_used = 0;            // 3 per closed sample: start, after the classify, end
+    std::vector<bool> ev_mid;      // per closed sample: the middle event was recorded
     // host round trip (upe_gpu_process_host): copy streams and three device slots
     hipStream_t s_in = nullptr, s_out = nullptr;
     struct HostSlot {
@@ -2458,6 +2464,12 @@ uint32_t resident_grid(upe_gpu_ctx* c, int var, size_t lds, hipStream_t s) {
 extern "C" {
 
 const char* upe_gpu_last_error(void) { return g_err.c_str(); }
+
+// For the library's C parts (upe_worker.c): set the calling thread's message, return -1.  Not
+// declared in include/upe_gpu.h and not exported.
+__attribute__((visibility("hidden"))) int upe_gpu_set_last_error(const char* msg) {
+    return fail(msg ? msg : "");
+}
 
 int upe_gpu_device_count(void) {
     int n = 0;
@@ -2983,14 +2995,17 @@ extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, s
     // a fresh, zeroed rule_stats of the new capacity; the old table's per-index totals dropped
     unsigned long long* fresh = nullptr;
     HIP_TRY(hipMalloc(&fresh, rule_capacity * 2 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(fresh, 0, rule_capacity * 2 * sizeof(unsigned long long)));
+    if (order_on(c, c->stream) != 0) return -1;
+    HIP_TRY(hipMemsetAsync(fresh, 0, rule_capacity * 2 * sizeof(unsigned long long), c->stream));
+    if (c->stats_idx)
+        HIP_TRY(hipMemsetAsync(c->stats_idx, 0,
+                               (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long),
+                               c->stream));
+    HIP_TRY(hipMemsetAsync(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->stats) (void)hipFree(c->stats);
     c->stats = fresh;
     c->cap = rule_capacity;
-    if (c->stats_idx)
-        HIP_TRY(hipMemset(c->stats_idx, 0,
-                          (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats)));
     c->rinfo_host.clear();   // nothing of the old table is left to credit
     if (publish(c) != 0) return -1;
     return upe_gpu_load_rules(c, rules, count);
@@ -3180,7 +3195,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
                       (c->timing_calls % c->timing_every) == c->timing_phase;
     if (c->timing) ++c->timing_calls;
     if (open) {
-        while (c->ev.size() < c->ev_used + 2) {
+        while (c->ev.size() < c->ev_used + 3) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             c->ev.push_back(e);
@@ -3329,7 +3344,12 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     HIP_TRY(hipGetLastError());
     c->last_var = var;
     c->last_grid = grid;
-    if (!lds_stats && n > 0 && !(kAblate & 4)) {
+    const bool group_by = !lds_stats && n > 0 && !(kAblate & 4);
+    // the sample's middle event, between the classify launch and the group-by (last call of the
+    // sample only; launches without a group-by have none)
+    const bool mid = c->t_left == 1 && group_by;
+    if (mid) HIP_TRY(hipEventRecord(c->ev[c->ev_used + 1], s));
+    if (group_by) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
         // kHistChunkMin) while the grid has fewer than about kHistTarget workgroups
         const uint32_t range = c->nrules_pad < kHistRange ? c->nrules_pad : kHistRange;
@@ -3361,8 +3381,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         HIP_TRY(hipGetLastError());
     }
     if (c->t_left && --c->t_left == 0) {
-        HIP_TRY(hipEventRecord(c->ev[c->ev_used + 1], s));
-        c->ev_used += 2;
+        HIP_TRY(hipEventRecord(c->ev[c->ev_used + 2], s));
+        c->ev_mid.push_back(mid);
+        c->ev_used += 3;
         c->timing_launches += c->timing_span;
     }
     ++c->k;
@@ -4033,6 +4054,7 @@ int upe_gpu_timing_span(upe_gpu_ctx_t* c, int every, int span) {
     DEV_SCOPE(c->device);
     HIP_TRY(hipDeviceSynchronize());
     c->ev_used = 0;   // the pool is kept for reuse
+    c->ev_mid.clear();
     c->timing = every > 0;
     c->timing_every = every > 0 ? (uint32_t)every : 1u;
     c->timing_phase = c->timing_every / 2;   // not the first call: it starts from an idle queue
@@ -4052,11 +4074,17 @@ int upe_gpu_timing_read(upe_gpu_ctx_t* c, double* classify_ms, double* finalize_
     if (!c) return fail("null context");
     DEV_SCOPE(c->device);
     double a = 0, b = 0;
-    for (size_t j = 0; j + 2 <= c->ev_used; j += 2) {
-        HIP_TRY(hipEventSynchronize(c->ev[j + 1]));
-        float x = 0;
-        HIP_TRY(hipEventElapsedTime(&x, c->ev[j], c->ev[j + 1]));
+    for (size_t j = 0, k = 0; j + 3 <= c->ev_used; j += 3, ++k) {
+        HIP_TRY(hipEventSynchronize(c->ev[j + 2]));
+        float x = 0, y = 0;
+        if (c->ev_mid[k]) {
+            HIP_TRY(hipEventElapsedTime(&x, c->ev[j], c->ev[j + 1]));
+            HIP_TRY(hipEventElapsedTime(&y, c->ev[j + 1], c->ev[j + 2]));
+        } else {
+            HIP_TRY(hipEventElapsedTime(&x, c->ev[j], c->ev[j + 2]));
+        }
         a += x;
+        b += y;
     }
     if (classify_ms) *classify_ms = a;
     if (finalize_ms) *finalize_ms = b;

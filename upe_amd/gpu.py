@@ -36,6 +36,36 @@ TX_BATCH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
                                ctypes.c_int)
 
 
+# upe_worker_ops_t callbacks (include/upe_gpu.h): the callees of the reference's worker_main
+_VP, _U8P = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)
+POP_FN = ctypes.CFUNCTYPE(ctypes.c_uint, _VP, ctypes.POINTER(_VP), ctypes.c_uint)
+STOP_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP)
+DATA_FN = ctypes.CFUNCTYPE(_VP, _VP, _VP)
+LEN_FN = ctypes.CFUNCTYPE(ctypes.c_size_t, _VP, _VP)
+FREE_FN = ctypes.CFUNCTYPE(None, _VP, _VP)
+TX_SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, ctypes.c_size_t)
+ARP_UPDATE_FN = ctypes.CFUNCTYPE(None, _VP, ctypes.c_uint32, _U8P)
+NDP_UPDATE_FN = ctypes.CFUNCTYPE(None, _VP, _U8P, _U8P)
+CTX_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP)
+POLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP)
+PUBLISH_FN = ctypes.CFUNCTYPE(None, _VP, _VP, _VP)
+
+
+class WorkerOps(ctypes.Structure):
+    """upe_worker_ops_t."""
+    _fields_ = [("pop_burst", POP_FN), ("stop", STOP_FN), ("data", DATA_FN), ("len", LEN_FN),
+                ("free_buf", FREE_FN), ("tx_send", TX_SEND_FN), ("tx_send_batch", TX_BATCH_FN),
+                ("arp_update", ARP_UPDATE_FN), ("ndp_update", NDP_UPDATE_FN),
+                ("load_neigh", CTX_FN), ("poll", POLL_FN), ("sync", CTX_FN),
+                ("publish", PUBLISH_FN)]
+
+
+class WorkerCfg(ctypes.Structure):
+    """upe_worker_cfg_t."""
+    _fields_ = [("batch", ctypes.c_size_t), ("burst", ctypes.c_uint), ("pool_base", _VP),
+                ("idle_ns", ctypes.c_uint)]
+
+
 class QueueBatch(ctypes.Structure):
     """upe_gpu_batch_t (include/upe_gpu.h)."""
     _fields_ = [("frames", ctypes.c_void_p), ("desc", ctypes.c_void_p),
@@ -99,6 +129,8 @@ def _load() -> ctypes.CDLL:
         "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
         "upe_gpu_process_split_emit": (I, [P, P, P, P, P, P, SZ, P]),
         "upe_gpu_process_split_batches_emit": (I, [P, P, P, P, P, P, SZ, SZ, P]),
+        "upe_gpu_worker_run": (I, [P, ctypes.POINTER(WorkerOps), P, ctypes.POINTER(WorkerCfg),
+                                   P]),
     }
     sig.update({
         "upe_rules_load_ini": (I, [ctypes.c_char_p, P, SZ, P]),
@@ -135,7 +167,8 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
-            "upe_tx_flush", "upe_gpu_process_split_emit", "upe_gpu_process_split_batches_emit")
+            "upe_tx_flush", "upe_gpu_process_split_emit", "upe_gpu_process_split_batches_emit",
+            "upe_gpu_worker_run")
 
 
 def _check(rc: int, what: str) -> None:

@@ -238,8 +238,10 @@ def pack_frames(hdr: np.ndarray, lens: np.ndarray, stride: int | None = None,
     keep = np.minimum(lens, w)
     if stride is not None and stride >= w:
         view = buf[: n * stride].reshape(n, stride)
-        m = np.arange(w)[None, :] < keep[:, None]
-        view[:, :w] = np.where(m, hdr, 0)
+        cols = np.arange(w, dtype=np.int64)[None, :]
+        for s in range(0, n, 1 << 18):   # chunks: no full-size mask or temporary
+            e = min(n, s + (1 << 18))
+            np.multiply(hdr[s:e], cols < keep[s:e, None], out=view[s:e, :w], casting="unsafe")
     else:
         chunk = 1 << 16
         cols = np.arange(w)
