@@ -7,7 +7,7 @@ from __future__ import annotations
 import numpy as np
 
 from upe_amd import synth
-from upe_amd.layout import ACT_DROP, ACT_FWD
+from upe_amd.layout import ACT_DROP, ACT_FWD, RULE_DTYPE
 
 CASES = {
     # name: (workload maker, packets, reload point, rule capacity after the reload)
@@ -29,7 +29,10 @@ def reloaded_rules(rules: np.ndarray, seed: int) -> np.ndarray:
     r = np.delete(r, int(rng.integers(0, len(r))))
     extra = np.zeros(1, r.dtype)
     extra[0] = synth.make_rule(1, ACT_FWD, ip_ver=4, proto=17, dport=53)
-    return np.concatenate([extra, r])
+    # (concatenate drops the structured dtype's padding: back to the 92-byte rule_t layout)
+    out = np.ascontiguousarray(np.concatenate([extra, r]).astype(RULE_DTYPE))
+    assert out.dtype.itemsize == 92
+    return out
 
 
 def case(name: str):

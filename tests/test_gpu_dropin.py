@@ -18,7 +18,7 @@ import pytest
 
 import oracle
 from upe_amd import synth
-from upe_amd.layout import RULE_STAT_DTYPE, V_FWD, desc_lens, desc_offsets
+from upe_amd.layout import RULE_DTYPE, RULE_STAT_DTYPE, V_FWD, desc_lens, desc_offsets
 
 pytestmark = pytest.mark.gpu
 
@@ -55,7 +55,7 @@ def _dropin(wl, mapped, reload=None):
     sizes, tx packet indexes, reply packet indexes)."""
     lib = _lib()
     lib.upe_dropin_set_mapped(1 if mapped else 0)
-    rules = np.ascontiguousarray(wl.rules)
+    rules = np.ascontiguousarray(wl.rules, dtype=RULE_DTYPE)
     eth = np.frombuffer(bytes(wl.eth_addr), np.uint8).copy()
     counters = np.zeros(5, np.uint64)
     cap_out = reload[1] if reload else wl.capacity
@@ -66,7 +66,7 @@ def _dropin(wl, mapped, reload=None):
     cap = wl.n + 16
     pops, sizes, tx, replies = (np.zeros(cap, np.uint32) for _ in range(4))
     log_n = np.zeros(4, np.uint64)
-    rb = np.ascontiguousarray(reload[0]) if reload else None
+    rb = np.ascontiguousarray(reload[0], dtype=RULE_DTYPE) if reload else None
     rc = lib.upe_dropin_run(_p(rules), len(rules), wl.capacity, _p(wl.arp), len(wl.arp),
                             _p(wl.ndp), len(wl.ndp), _p(eth), wl.ip4_addr, _p(wl.frames),
                             _p(wl.desc), wl.n, 0, _p(counters), _p(stats), _p(frames), _p(arp),

@@ -77,7 +77,7 @@ def ipv6_mask(prefix: int) -> bytes:
 def build_rule_table(rules: np.ndarray) -> np.ndarray:
     """Final rt->rules after rule_table_add() of `rules` in order: rule_id = insertion index,
     wildcard (all-zero mask) addresses zeroed for ip_ver 4/6, sorted by (priority, rule_id)."""
-    r = rules.copy()
+    r = np.ascontiguousarray(rules).astype(RULE_DTYPE)   # (the 92-byte rule_t layout, padded)
     r["rule_id"] = np.arange(len(r), dtype=np.uint32)
     v4 = r["ip_ver"] == 4
     v6 = r["ip_ver"] == 6
