@@ -297,8 +297,12 @@ int upe_gpu_process_split_batches_emit(upe_gpu_ctx_t *ctx, const uint8_t *const 
  * ring's start.  n a multiple of 1024, n * count <= 2^24.  d_done_ns (optional, device or
  * host-mapped, count entries): for each batch, the time (ns) from the launch's first workgroup
  * to the moment its last workgroup had issued the batch's last stores — per-batch completion
- * latency — or 0 where not stamped (stamps need a linear-scan table and batches of at least
- * one tile per persistent workgroup, 256k packets on MI355X).  Asynchronous on `stream`. */
+ * latency — or 0 where not stamped (stamps need a linear-scan table, batches of at least
+ * one tile per persistent workgroup, 256k packets on MI355X, and at most 64 batches per
+ * workgroup's share).  A stamp excludes the launch's final repair of look-back candidates that
+ * waves deferred (launch_info().deferred > 0, only when another kernel holds CUs): such a
+ * batch's last verdicts and records are final when the launch completes, not at its stamp.
+ * Asynchronous on `stream`. */
 int upe_gpu_process_ring_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                               uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n, size_t count,
                               uint64_t *d_done_ns, void *stream);

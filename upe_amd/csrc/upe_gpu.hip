@@ -406,6 +406,14 @@ __device__ __forceinline__ uint32_t be16_lo(uint32_t x) {             // BE u16 
 }
 // RFC 1071 fold of a sum of native-LE u16 words held as a sum of u32 (u32 = lo + hi * 2^16,
 // and 2^16 == 1 in one's-complement arithmetic), complemented: src/parser.c:137-169.
+// v_bfi_b32 with a per-lane all-ones / all-zeros mask in a VGPR: a where m is set, else b (a
+// select the compiler cannot turn into an indexed load of the array a and b come from, and one
+// that needs no SGPR lane mask)
+__device__ __forceinline__ uint32_t vsel(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ uint32_t csum_fold(unsigned long long sum) {
     uint32_t f = (uint32_t)(sum & 0xFFFFFFFFull) + (uint32_t)(sum >> 32);
     f += (uint32_t)(sum & 0xFFFFFFFFull) > f ? 1u : 0u;            // end-around carry
@@ -817,6 +825,7 @@ struct Parsed {
 struct Port {
     uint32_t mac_lo, mac_hi, ip4;
 };
+template <bool kBarrel>
 __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, Parsed& r,
                                              const uint32_t (&win)[24]) {
     r.ok = false; r.consumed = false; r.v6 = false; r.flags = 0;
@@ -907,15 +916,43 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
                 r.s[0] = bswap32(at2(w[7], w[6]));                           // bytes 26..29
                 r.d[0] = bswap32(at2(w[8], w[7]));                           // bytes 30..33
                 const uint32_t l4len = len - 14 - hl;
-                // L4 starts at byte 14 + 4 * ihl = 4 * (ihl + 3) + 2 (registers are not
-                // indexable: select the window by IHL)
-                uint32_t l4w0 = 0, l4w1 = 0, l4w3 = 0;
+                // L4 starts at byte 14 + 4 * ihl = 4 * (ihl + 3) + 2, i.e. in word ihl + 3, and
+                // registers are not indexable: l4 words from w[ihl + 3 .. ihl + 7], and x0 =
+                // w[ihl + 3] (the checksum's last half word), selected by IHL
+                uint32_t l4w0 = 0, l4w1 = 0, l4w3 = 0, x0 = 0;
+                if constexpr (kBarrel) {
+                    // a four-stage barrel shift by ihl - 5 (31 selects; ihl < 5 fails the parse
+                    // above, so only shifts 0..10 matter).  Tuple-space kernels only: in the scan
+                    // kernels it measured slower for config B, whose waves never run this path
+                    // (24.5 -> 26.7 us, an allocation effect; profiles/r04/v4_wave_general_ab.txt)
+                    const uint32_t sh = ihl - 5u;
+                    const uint32_t m8 = (uint32_t)((int32_t)(sh << 28) >> 31);
+                    const uint32_t m4 = (uint32_t)((int32_t)(sh << 29) >> 31);
+                    const uint32_t m2 = (uint32_t)((int32_t)(sh << 30) >> 31);
+                    const uint32_t m1 = (uint32_t)((int32_t)(sh << 31) >> 31);
+                    uint32_t y[12], z[8], u[6], x[5];
 #pragma unroll
-                for (int h = 5; h <= 15; ++h) {
-                    if ((int)ihl == h) {
-                        l4w0 = at2(w[h + 4], w[h + 3]);
-                        l4w1 = at2(w[h + 5], w[h + 4]);
-                        l4w3 = at2(w[h + 7], w[h + 6]);
+                    for (int k = 0; k < 12; ++k)
+                        y[k] = 16 + k < 24 ? vsel(m8, w[16 + k < 24 ? 16 + k : 0], w[8 + k]) : w[8 + k];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) z[k] = vsel(m4, y[k + 4], y[k]);
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) u[k] = vsel(m2, z[k + 2], z[k]);
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) x[k] = vsel(m1, u[k + 1], u[k]);
+                    l4w0 = at2(x[1], x[0]);
+                    l4w1 = at2(x[2], x[1]);
+                    l4w3 = at2(x[4], x[3]);
+                    x0 = x[0];
+                } else {
+#pragma unroll
+                    for (int h = 5; h <= 15; ++h) {
+                        if ((int)ihl == h) {
+                            l4w0 = at2(w[h + 4], w[h + 3]);
+                            l4w1 = at2(w[h + 5], w[h + 4]);
+                            l4w3 = at2(w[h + 7], w[h + 6]);
+                            x0 = w[h + 3];
+                        }
                     }
                 }
                 if (r.proto == 17u) {
@@ -933,22 +970,41 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
                     r.dport = be16_lo(l4w0);                                 // type << 8 | code
                 }
                 // checksum over IHL*4 bytes with the TTL decremented and the field zeroed:
-                // sum of u16 words = (w3 >> 16) + w4 + ... + w[2 + ihl] + (w[3 + ihl] & 0xFFFF)
+                // sum of u16 words = (w3 >> 16) + w4 + ... + w[2 + ihl] + (w[3 + ihl] & 0xFFFF);
+                // words 7..2+ihl as the sum of their 16-bit halves (v_dot2_u32_u16 with a 0/1
+                // pair: congruent mod 0xFFFF, which is all the fold needs), w[3 + ihl] = x0
                 r.ttl = byte_of(w[5], 2);
                 const uint32_t w5n = (w[5] & 0xFF00FFFFu) | (((r.ttl - 1) & 0xFFu) << 16);
                 const uint32_t w6z = w[6] & 0xFFFF0000u;
-                unsigned long long sum = (w[3] >> 16) + (unsigned long long)w[4] + w5n + w6z;
+                typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+                uint32_t hs = x0 & 0xFFFFu;
 #pragma unroll
-                for (int k = 7; k <= 17; ++k)
-                    if ((uint32_t)k <= 2 + ihl) sum += w[k];
-#pragma unroll
-                for (int h = 5; h <= 15; ++h)
-                    if ((int)ihl == h) sum += w[3 + h] & 0xFFFFu;
+                for (int k = 7; k <= 17; ++k) {
+                    const ushort2_t one = {1, 1}, none = {0, 0};
+                    hs = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, w[k]),
+                                                (uint32_t)k <= 2 + ihl ? one : none, hs, false);
+                }
+                const unsigned long long sum = (w[3] >> 16) + (unsigned long long)w[4] + w5n + w6z + hs;
                 r.c1w1 = w5n;
                 r.c1w2 = w6z | csum_fold(sum);
             }
         } else if (is_v6 && len - 14 >= 40u) {
-            // (len >= 54: only a fast-path packet; reached here when len < 54 -> parse fails)
+            // as the fast path: next header byte 20, addresses 22..53, L4 at byte 54
+            r.proto = byte_of(w[5], 0);
+            r.s[0] = at2(w[6], w[5]);   r.s[1] = at2(w[7], w[6]);
+            r.s[2] = at2(w[8], w[7]);   r.s[3] = at2(w[9], w[8]);
+            r.d[0] = at2(w[10], w[9]);  r.d[1] = at2(w[11], w[10]);
+            r.d[2] = at2(w[12], w[11]); r.d[3] = at2(w[13], w[12]);
+            const uint32_t l4a = at2(w[14], w[13]), l4b = at2(w[15], w[14]);
+            const uint32_t l4c = at2(w[17], w[16]);
+            const uint32_t l4len = len - 54u;
+            const uint32_t thl = (byte_of(l4c, 0) >> 4) * 4;
+            const bool udp = r.proto == 17u, tcp = r.proto == 6u, icmp = r.proto == 1u;
+            r.ok = (udp || icmp) ? l4len >= 8u : tcp && l4len >= 20u && thl >= 20u && l4len >= thl;
+            r.sport = icmp ? be16_lo(l4b) : be16_lo(l4a);
+            r.dport = icmp ? be16_lo(l4a) : be16_lo(l4a >> 16);
+            r.ttl = byte_of(w[5], 1);
+            r.c1w1 = (w[5] & 0xFFFF00FFu) | (((r.ttl - 1) & 0xFFu) << 8);
         }
     }
 }
@@ -1009,7 +1065,10 @@ __device__ uint32_t lookback(const uint32_t* lb, uint32_t chunk, uint32_t tag, u
 // has been processed by now, so every flag word of this launch is written or about to land.  F4 /
 // F6 = the first chunk holding a miss-then-hit packet of each family; a deferred candidate of
 // chunk c takes the starting entry's MAC iff F >= c (the earlier lanes of its own chunk were
-// checked when it deferred).  entries[e] = packet index | family << 31 (1 = IPv6).
+// checked when it deferred).  entries[e] = packet index | family << 31 (1 = IPv6).  Plain
+// stores suffice: launches on a context are ordered (no launch of the context starts before this
+// one's end-of-kernel writeback), and nothing else in this launch writes these words after the
+// deferring wave did.
 constexpr int kRepairUnroll = 4;
 struct Repair {
     uint32_t mac4_lo, mac4_hi, mac6_lo, mac6_hi;   // the batch's starting L1 entries' MACs
@@ -1356,55 +1415,67 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (!folded) fold_start();
 
         if (first) STAMP_VM(2);
-        // ---- fast path: option-less IPv4 / IPv6 ----
+        // ---- fast path (option-less IPv4 / IPv6) or general path, chosen per wave ----
         const uint32_t e12 = w[3] & 0xFFFFu;          // bytes 12,13 (ethertype, byte-swapped)
         const bool fast4 = live && len >= 34u && e12 == 0x0008u && byte_of(w[3], 2) == 0x45u;
         const bool fast6 = live && len >= 54u && e12 == 0xDD86u;
-        Parsed r;
-        r.ok = false; r.consumed = false; r.v6 = fast6; r.flags = 0;
-        r.proto = fast6 ? byte_of(w[5], 0) : byte_of(w[5], 3);              // byte 20 / 23
-        // addresses: v4 host order in word 0 (src/parser.c:40-41); v6 wire bytes
-        r.s[0] = fast6 ? at2(w[6], w[5]) : bswap32(at2(w[7], w[6]));
-        r.d[0] = fast6 ? at2(w[10], w[9]) : bswap32(at2(w[8], w[7]));
-        r.s[1] = at2(w[7], w[6]);  r.s[2] = at2(w[8], w[7]);  r.s[3] = at2(w[9], w[8]);
-        r.d[1] = at2(w[11], w[10]); r.d[2] = at2(w[12], w[11]); r.d[3] = at2(w[13], w[12]);
-        {
-            // L4 at byte 34 (v4) or 54 (v6), both 2 mod 4
-            const uint32_t l4a = fast6 ? at2(w[14], w[13]) : at2(w[9], w[8]);     // L4 0..3
-            const uint32_t l4b = fast6 ? at2(w[15], w[14]) : at2(w[10], w[9]);    // L4 4..7
-            const uint32_t l4c = fast6 ? at2(w[17], w[16]) : at2(w[12], w[11]);   // L4 12..15
-            const uint32_t l4len = len - (fast6 ? 54u : 34u);
-            const uint32_t thl = (byte_of(l4c, 0) >> 4) * 4;
-            const bool udp = r.proto == 17u, tcp = r.proto == 6u, icmp = r.proto == 1u;
-            r.ok = (fast4 || fast6) &&
-                   ((udp || icmp) ? l4len >= 8u
-                                  : tcp && l4len >= 20u && thl >= 20u && l4len >= thl);
-            r.sport = icmp ? be16_lo(l4b) : be16_lo(l4a);                  // icmp: id
-            r.dport = icmp ? be16_lo(l4a) : be16_lo(l4a >> 16);            // type << 8 | code
-            // NDP NS / NA, consumed by handle_control_packet (src/worker.c:57-100)
-            r.consumed = fast6 && len >= 78u && r.proto == 58u &&
-                         ((l4a & 0xFFu) == 135u || (l4a & 0xFFu) == 136u);
-        }
-        // forward rewrite of bytes 20..27: v4 ttl-- and checksum over the 20-byte header
-        // (src/worker.c:174-176, src/parser.c:137-169, stored LE), v6 hop-- (src/worker.c:213)
-        r.ttl = fast6 ? byte_of(w[5], 1) : byte_of(w[5], 2);               // byte 21 / 22
-        if (fast6) {
-            r.c1w1 = (w[5] & 0xFFFF00FFu) | (((r.ttl - 1) & 0xFFu) << 8);
-            r.c1w2 = w[6];
-        } else {
-            const uint32_t w5n = (w[5] & 0xFF00FFFFu) | (((r.ttl - 1) & 0xFFu) << 16);
-            const uint32_t w6z = w[6] & 0xFFFF0000u;
-            const unsigned long long sum = (unsigned long long)(w[3] >> 16) + w[4] + w5n + w6z +
-                                           w[7] + (w[8] & 0xFFFFu);
-            r.c1w1 = w5n;
-            r.c1w2 = w6z | csum_fold(sum);
-        }
-
-        // ---- general path, for the waves that hold anything else ----
         const bool slow = live && !fast4 && !fast6 && !(kAblate & 16);
-        if (__any(slow) && slow) {
+        Parsed r;
+        // Tuple-space kernels (large tables): a wave holding any other frame parses all 64 on
+        // the general path, which gives the fast path's results for the fast path's frames — one
+        // parse per wave instead of both (config D: IPv4 options, VLAN tags and malformed headers
+        // put such a frame in nearly every wave; classify 651 -> 641 us per 16M).  The scan
+        // kernels keep the fast path for every wave and the general path for the lanes that need
+        // it: there the merged form costs registers (C's emit kernel spilled 12 VGPRs to scratch,
+        // 39.9 -> 44.3 us; B 24.7 -> 25.1; profiles/r04/v4_wave_general_ab.txt).
+        constexpr bool kWaveGeneral = kTssMode;
+        const bool wave_general = kWaveGeneral && __any(slow);
+        if (wave_general) {
+            general_path<kTssMode>(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, r, w);
+        } else {
+            r.ok = false; r.consumed = false; r.v6 = fast6; r.flags = 0;
+            r.proto = fast6 ? byte_of(w[5], 0) : byte_of(w[5], 3);              // byte 20 / 23
+            // addresses: v4 host order in word 0 (src/parser.c:40-41); v6 wire bytes
+            r.s[0] = fast6 ? at2(w[6], w[5]) : bswap32(at2(w[7], w[6]));
+            r.d[0] = fast6 ? at2(w[10], w[9]) : bswap32(at2(w[8], w[7]));
+            r.s[1] = at2(w[7], w[6]);  r.s[2] = at2(w[8], w[7]);  r.s[3] = at2(w[9], w[8]);
+            r.d[1] = at2(w[11], w[10]); r.d[2] = at2(w[12], w[11]); r.d[3] = at2(w[13], w[12]);
+            {
+                // L4 at byte 34 (v4) or 54 (v6), both 2 mod 4
+                const uint32_t l4a = fast6 ? at2(w[14], w[13]) : at2(w[9], w[8]);     // L4 0..3
+                const uint32_t l4b = fast6 ? at2(w[15], w[14]) : at2(w[10], w[9]);    // L4 4..7
+                const uint32_t l4c = fast6 ? at2(w[17], w[16]) : at2(w[12], w[11]);   // L4 12..15
+                const uint32_t l4len = len - (fast6 ? 54u : 34u);
+                const uint32_t thl = (byte_of(l4c, 0) >> 4) * 4;
+                const bool udp = r.proto == 17u, tcp = r.proto == 6u, icmp = r.proto == 1u;
+                r.ok = (fast4 || fast6) &&
+                       ((udp || icmp) ? l4len >= 8u
+                                      : tcp && l4len >= 20u && thl >= 20u && l4len >= thl);
+                r.sport = icmp ? be16_lo(l4b) : be16_lo(l4a);                  // icmp: id
+                r.dport = icmp ? be16_lo(l4a) : be16_lo(l4a >> 16);            // type << 8 | code
+                // NDP NS / NA, consumed by handle_control_packet (src/worker.c:57-100)
+                r.consumed = fast6 && len >= 78u && r.proto == 58u &&
+                             ((l4a & 0xFFu) == 135u || (l4a & 0xFFu) == 136u);
+            }
+            // forward rewrite of bytes 20..27: v4 ttl-- and checksum over the 20-byte header
+            // (src/worker.c:174-176, src/parser.c:137-169, stored LE), v6 hop-- (src/worker.c:213)
+            r.ttl = fast6 ? byte_of(w[5], 1) : byte_of(w[5], 2);               // byte 21 / 22
+            if (fast6) {
+                r.c1w1 = (w[5] & 0xFFFF00FFu) | (((r.ttl - 1) & 0xFFu) << 8);
+                r.c1w2 = w[6];
+            } else {
+                const uint32_t w5n = (w[5] & 0xFF00FFFFu) | (((r.ttl - 1) & 0xFFu) << 16);
+                const uint32_t w6z = w[6] & 0xFFFF0000u;
+                const unsigned long long sum = (unsigned long long)(w[3] >> 16) + w[4] + w5n + w6z +
+                                               w[7] + (w[8] & 0xFFFFu);
+                r.c1w1 = w5n;
+                r.c1w2 = w6z | csum_fold(sum);
+            }
+
+        }
+        if (!kWaveGeneral && __any(slow) && slow) {
             Parsed g;
-            general_path(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g, w);
+            general_path<kTssMode>(Port{a.port_mac_lo, a.port_mac_hi, a.port_ip4}, p, len, g, w);
             r = g;
         }
 
