@@ -431,3 +431,21 @@ def test_config_a_pcap_replay(gpu_worker_factory, tmp_path):
 
     for o, go, ln in zip(desc_offsets(desc), desc_offsets(wl.desc), desc_lens(desc)):
         assert np.array_equal(out_frames[o:o + ln], ref["frames"][go:go + ln])
+
+
+@pytest.mark.parametrize("emit", [False, True])
+@pytest.mark.parametrize("n_rules", [4100, 65536, 65540, 1 << 17])
+def test_group_by_key_forms(gpu_worker_factory, n_rules, emit):
+    """rule_stats of tables past the LDS histogram: up to 64k rules the group-by reads one
+    4-byte key per packet (rule << 16 | length) the classify pass leaves; past that the verdict
+    word and a 2-byte length — both forms, and the boundary between them, against the oracle."""
+    wl = synth.config_d(n=20_000, seed=91, n_rules=n_rules)
+    frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl, emit=emit)
+    key = ("group_by", n_rules)
+    if key not in _D_CACHE:   # up to ~12 s of oracle scans, shared by both modes
+        _D_CACHE[key] = oracle.run_restated(wl)
+    r = _D_CACHE[key]
+    assert np.array_equal(verdict, r.verdict)
+    assert np.array_equal(stats, r.rule_stats)
+    assert counters.tobytes() == r.counters.tobytes()
+    assert np.array_equal(frames, r.frames)

@@ -298,7 +298,9 @@ struct Args {
     uint32_t ndp_lds;                // NDP index staged in LDS (slots, 2 x uint4 each), 0 = not
     uint32_t fp_lds;                 // staged fingerprints in LDS (uint4 of tfs), 0 = none
     uint32_t* flow_hash;             // optional [n]: flow_hash of each parsed packet (RSS)
-    uint16_t* lens16;                // optional [n]: frame lengths for the rule_stats group-by
+    void* gb;                        // optional [n]: what the rule_stats group-by reads beside
+                                     // the verdicts (gb_packed: u32 keys, else u16 lengths)
+    uint32_t gb_packed;              // 1: gb[i] = matched ? sorted rule index << 16 | len : 0
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
     // this batch's slots of the between-batch state (DevState comment) follow from k6 = k % 6
     // (pointers computed where they are used: the kernel's scalar registers are scarce)
@@ -1667,9 +1669,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (live)   // written through (sc1): no dirty lines left for the boundary
             __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-        // 2 B/packet for upe_rule_hist (lean linear-scan launches never have the array; the
+        // the side array upe_rule_hist reads (lean linear-scan launches never have it; the
         // tuple-space tables it serves always do)
-        if ((kTssMode || !kLean) && a.lens16 && live) a.lens16[i] = (uint16_t)len;
+        if ((kTssMode || !kLean) && a.gb && live) {
+            // tables of up to 64k rules: the rule and the length in one 4-byte key, so that the
+            // group-by reads 4 bytes per packet per rule range instead of verdict + length (6)
+            if (a.gb_packed)
+                static_cast<uint32_t*>(a.gb)[i] = rbits ? ((rbits << 8) - 0x10000u) | len : 0u;
+            else
+                static_cast<uint16_t*>(a.gb)[i] = (uint16_t)len;
+        }
         if (!kLean && a.flow_hash && live) {
             // software RSS in the same pass: flow_hash (reference src/parser.c:113-135) of the
             // key parse_flow_key gives the RX thread (src/rx_pcap.c:71-72), 0 if it fails
@@ -1860,8 +1869,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
 // rule falls in range y in LDS bins (packets << 40 | bytes, which cannot overflow: a chunk holds
 // at most 2^24 packets of at most 65535 bytes), then writes the bins densely into per-chunk
 // partials that upe_hist_reduce sums (device atomics per nonzero bin, measured in round 2, were
-// no faster and needed a packed staging array).  Every range re-reads its chunk (verdict word + the 2-byte length the classify
-// pass left), so ranges are as wide as LDS allows; 1024-thread workgroups with sixteen packets
+// no faster and needed a packed staging array).  Every range re-reads its chunk (for tables of up
+// to 64k rules the 4-byte key the classify pass left — rule << 16 | length, round 4: 6 -> 4 bytes
+// per packet per range; larger ones the verdict word + a 2-byte length), so ranges are as wide
+// as LDS allows; 1024-thread workgroups with sixteen packets
 // per thread per round keep enough loads in flight (config D: 256-thread workgroups with four
 // packets a round spent ~300 us per 16M batch waiting on them; eight a round 69.5 us, sixteen
 // 62.6 us, thirty-two slower again).
@@ -1883,8 +1894,9 @@ constexpr int kHistBlock = 1024;
 constexpr int kHistPer = UPE_HIST_PER;   // packets per thread per round (a multiple of 8)
 static_assert(kHistPer % 8 == 0 && 8192 % (kHistPer * 1) == 0, "group-by rounds stay 16-byte aligned");
 
+template <bool kPacked>
 __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verdict,
-                                                            const uint16_t* lens, uint32_t n,
+                                                            const void* gb, uint32_t n,
                                                             uint32_t nrules,
                                                             unsigned long long* part,
                                                             uint32_t chunk, uint32_t range) {
@@ -1894,36 +1906,46 @@ __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verd
     for (uint32_t k = threadIdx.x; k < range; k += kHistBlock) h[k] = 0;
     __syncthreads();
     const uint32_t pend = n - p0 < chunk ? n : p0 + chunk;
-    // kHistPer packets per thread per round: kHistPer / 4 16-byte verdict loads and kHistPer / 8
-    // 16-byte length loads, all issued before the first bin update (chunks start at multiples of
-    // 8192, so full groups are 16-byte aligned)
+    // kHistPer packets per thread per round, all loads issued before the first bin update
+    // (chunks start at multiples of 8192, so full groups are 16-byte aligned).  Packed keys:
+    // kHistPer / 4 16-byte key loads (rule index << 16 | len, 0 = not counted); otherwise
+    // kHistPer / 4 verdict loads and kHistPer / 8 length loads.
+    const uint32_t* keys = static_cast<const uint32_t*>(gb);
+    const uint16_t* lens = static_cast<const uint16_t*>(gb);
     for (uint32_t i = p0 + kHistPer * threadIdx.x; i < pend; i += kHistPer * kHistBlock) {
-        uint32_t v[kHistPer], len[kHistPer];
+        uint32_t rb[kHistPer], len[kHistPer];   // rule index + 1 (0 = none), length
         if (i + kHistPer <= pend) {
 #pragma unroll
             for (int q = 0; q < kHistPer / 4; ++q) {
-                const uint4 a0 = *reinterpret_cast<const uint4*>(verdict + i + 4 * q);
-                v[4 * q + 0] = a0.x; v[4 * q + 1] = a0.y; v[4 * q + 2] = a0.z; v[4 * q + 3] = a0.w;
+                const uint4 a0 = *reinterpret_cast<const uint4*>((kPacked ? keys : verdict) + i + 4 * q);
+                rb[4 * q + 0] = a0.x; rb[4 * q + 1] = a0.y; rb[4 * q + 2] = a0.z; rb[4 * q + 3] = a0.w;
             }
+            if (!kPacked) {
 #pragma unroll
-            for (int q = 0; q < kHistPer / 8; ++q) {
-                const uint4 l = *reinterpret_cast<const uint4*>(lens + i + 8 * q);
-                len[8 * q + 0] = l.x & 0xFFFFu; len[8 * q + 1] = l.x >> 16;
-                len[8 * q + 2] = l.y & 0xFFFFu; len[8 * q + 3] = l.y >> 16;
-                len[8 * q + 4] = l.z & 0xFFFFu; len[8 * q + 5] = l.z >> 16;
-                len[8 * q + 6] = l.w & 0xFFFFu; len[8 * q + 7] = l.w >> 16;
+                for (int q = 0; q < kHistPer / 8; ++q) {
+                    const uint4 l = *reinterpret_cast<const uint4*>(lens + i + 8 * q);
+                    len[8 * q + 0] = l.x & 0xFFFFu; len[8 * q + 1] = l.x >> 16;
+                    len[8 * q + 2] = l.y & 0xFFFFu; len[8 * q + 3] = l.y >> 16;
+                    len[8 * q + 4] = l.z & 0xFFFFu; len[8 * q + 5] = l.z >> 16;
+                    len[8 * q + 6] = l.w & 0xFFFFu; len[8 * q + 7] = l.w >> 16;
+                }
             }
         } else {
 #pragma unroll
             for (int j = 0; j < kHistPer; ++j) {
-                v[j] = i + j < pend ? verdict[i + j] : 0u;
-                len[j] = i + j < pend ? (uint32_t)lens[i + j] : 0u;
+                rb[j] = i + j < pend ? (kPacked ? keys : verdict)[i + j] : 0u;
+                if (!kPacked) len[j] = i + j < pend ? (uint32_t)lens[i + j] : 0u;
             }
         }
 #pragma unroll
         for (int j = 0; j < kHistPer; ++j) {
-            const uint32_t rb = v[j] >> 8;   // matched rule's sorted index + 1, 0 = none
-            if (rb != 0 && rb - 1u - r0 < range) atomicAdd(&h[rb - 1u - r0], (1ull << 40) | len[j]);
+            if (kPacked) {
+                len[j] = rb[j] & 0xFFFFu;
+                rb[j] = len[j] ? (rb[j] >> 16) + 1u : 0u;
+            } else {
+                rb[j] >>= 8;   // matched rule's sorted index + 1, 0 = none
+            }
+            if (rb[j] != 0 && rb[j] - 1u - r0 < range) atomicAdd(&h[rb[j] - 1u - r0], (1ull << 40) | len[j]);
         }
     }
     __syncthreads();
@@ -1940,6 +1962,7 @@ __global__ void __launch_bounds__(kHistBlock) upe_rule_hist(const uint32_t* verd
 // word has exactly one writer in the launch, so the adds are plain.
 __global__ void __launch_bounds__(256) upe_hist_reduce(const unsigned long long* part,
                                                        uint32_t nchunks, uint32_t nrules,
+                                                       uint32_t nrules_pad,
                                                        unsigned long long* stats_idx) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= nrules) return;
@@ -1961,7 +1984,7 @@ __global__ void __launch_bounds__(256) upe_hist_reduce(const unsigned long long*
         by += b & ((1ull << 40) - 1);
     }
     if (pk) {
-        unsigned long long* o = stats_idx + (size_t)(blockIdx.y % kStatReps) * 2 * nrules + 2 * (size_t)r;
+        unsigned long long* o = stats_idx + (size_t)(blockIdx.y % kStatReps) * 2 * nrules_pad + 2 * (size_t)r;
         o[0] += pk;
         o[1] += by;
     }
@@ -2182,8 +2205,8 @@ struct upe_gpu_ctx {
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
     unsigned long long* hist_part = nullptr;   // [chunks][nrules_pad] dense group-by partials
     size_t hist_part_alloc = 0;
-    uint16_t* lens16 = nullptr;                // [lens_alloc] frame lengths (group-by tables)
-    size_t lens_alloc = 0;
+    void* gb = nullptr;                        // [gb_alloc] u32: group-by keys or u16 lengths
+    size_t gb_alloc = 0;
     std::vector<int2> rinfo_host;              // (action, rule_id) per sorted index
     // tuple-space index of large tables (null when the linear scan is used)
     TssGroup* tg4 = nullptr;
@@ -2710,7 +2733,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (!c) return;
     DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->lens16, c->arp, c->ndp, c->st, c->stats,
+    void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->gb, c->arp, c->ndp, c->st, c->stats,
                     c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs,
                     c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
@@ -3314,17 +3337,18 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.slab = slab;
     const bool emit = d_hdr != nullptr && n > 0;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
-    a.lens16 = nullptr;
+    a.gb = nullptr;
+    a.gb_packed = c->nrules <= 65536u ? 1u : 0u;   // sorted indexes of matches < nrules
     if (!lds_stats && n > 0 && !(kAblate & 4)) {
-        if (n > c->lens_alloc) {
-            if (c->lens16) (void)hipFree(c->lens16);
-            c->lens16 = nullptr;
-            c->lens_alloc = 0;
+        if (n > c->gb_alloc) {
+            if (c->gb) (void)hipFree(c->gb);
+            c->gb = nullptr;
+            c->gb_alloc = 0;
             const size_t want = (n + n / 4 + 64) & ~(size_t)3;
-            HIP_TRY(hipMalloc(&c->lens16, want * sizeof(uint16_t)));
-            c->lens_alloc = want;
+            HIP_TRY(hipMalloc(&c->gb, want * sizeof(uint32_t)));   // room for either form
+            c->gb_alloc = want;
         }
-        a.lens16 = c->lens16;
+        a.gb = c->gb;
     }
     const size_t hist = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
     // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
@@ -3348,7 +3372,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     }
     // the lean emit kernel when nothing it leaves out is needed (non-empty neighbour indexes
     // all in LDS, no flow_hash, no length side array)
-    const bool lean = !d_flow_hash && (c->tss || !a.lens16) &&
+    const bool lean = !d_flow_hash && (c->tss || !a.gb) &&
                       (arp_slots == 0 || a.arp_lds != 0) && (ndp_slots == 0 || a.ndp_lds != 0);
     // once a launch has been seen starting from agreeing L1 entries (or from an entry whose
     // family's index is empty), every later one does until the host changes tables or entries
@@ -3423,14 +3447,17 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     if (group_by) {
         // bins for up to kHistRange rules per workgroup; packet chunks halved (down to
         // kHistChunkMin) while the grid has fewer than about kHistTarget workgroups
-        const uint32_t range = c->nrules_pad < kHistRange ? c->nrules_pad : kHistRange;
-        const uint32_t nr = (c->nrules_pad + range - 1) / range;
+        // (over the rules that can match, sorted indexes 0..nrules-1: the padding block never
+        // does, and counting it cost config D a fifth range pass over the batch)
+        const uint32_t nrules = c->nrules ? c->nrules : 1u;
+        const uint32_t range = nrules < kHistRange ? nrules : kHistRange;
+        const uint32_t nr = (nrules + range - 1) / range;
         uint32_t chunk = kHistChunk;
         while (chunk > kHistChunkMin && ((n + chunk / 2 - 1) / (chunk / 2)) * nr <= kHistTarget)
             chunk >>= 1;
         const dim3 hg((uint32_t)((n + chunk - 1) / chunk), nr);
         // dense partials: one 8-byte bin per chunk and rule, summed by upe_hist_reduce
-        const size_t part_words = (size_t)hg.x * c->nrules_pad;
+        const size_t part_words = (size_t)hg.x * nrules;
         if (part_words > c->hist_part_alloc) {
             if (c->hist_part) (void)hipFree(c->hist_part);
             c->hist_part = nullptr;
@@ -3439,16 +3466,23 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             c->hist_part_alloc = part_words;
         }
         static std::atomic<uint64_t> hist_attr{0};   // 128 KB of dynamic LDS, once per device
-        if (!(hist_attr.fetch_or(1ull << (c->device & 63)) & (1ull << (c->device & 63))))
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_rule_hist),
+        if (!(hist_attr.fetch_or(1ull << (c->device & 63)) & (1ull << (c->device & 63)))) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_rule_hist<true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)(kHistRange * sizeof(unsigned long long)));
-        hipLaunchKernelGGL(upe_rule_hist, hg, dim3(kHistBlock), range * sizeof(unsigned long long), s,
-                           d_verdict, c->lens16, (uint32_t)n, c->nrules_pad, c->hist_part, chunk,
-                           range);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&upe_rule_hist<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(kHistRange * sizeof(unsigned long long)));
+        }
+        if (a.gb_packed)
+            hipLaunchKernelGGL(upe_rule_hist<true>, hg, dim3(kHistBlock), range * sizeof(unsigned long long), s,
+                               d_verdict, c->gb, (uint32_t)n, nrules, c->hist_part, chunk, range);
+        else
+            hipLaunchKernelGGL(upe_rule_hist<false>, hg, dim3(kHistBlock), range * sizeof(unsigned long long), s,
+                               d_verdict, c->gb, (uint32_t)n, nrules, c->hist_part, chunk, range);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(upe_hist_reduce, dim3((c->nrules_pad + 255) / 256, kStatReps),
-                           dim3(256), 0, s, c->hist_part, hg.x, c->nrules_pad, c->stats_idx);
+        hipLaunchKernelGGL(upe_hist_reduce, dim3((nrules + 255) / 256, kStatReps),
+                           dim3(256), 0, s, c->hist_part, hg.x, nrules, c->nrules_pad, c->stats_idx);
         HIP_TRY(hipGetLastError());
     }
     if (c->t_left && --c->t_left == 0) {
