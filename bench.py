@@ -360,7 +360,7 @@ def host_mapped(worker, wl, reps: int, emit: bool) -> dict:
 
 
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
-             copies_cap: int, split: bool = False) -> dict:
+             copies_cap: int) -> dict:
     """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
     timed the same way as `value`, on every rank at once after the main region, so that a
     multi-GPU run reports the 64 B and the IMIX rates at each N (BASELINE north_star).  Each rank
@@ -385,32 +385,16 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     base = pool.data_ptr()
-    rbase = rstride = 0
-    if split:
-        # header-split batches: each copy's first-64-byte rows beside its frames
-        rows = torch.from_numpy(synth.header_rows(wl).reshape(-1)).to(dev)
-        rstride = int(rows.numel())
-        rpool = torch.empty(copies * rstride, dtype=torch.uint8, device=dev)
-        for c in range(copies):
-            rpool[c * rstride:(c + 1) * rstride].copy_(rows)
-        del rows
-        rbase = rpool.data_ptr()
 
-    def run(k0: int, count: int, ptrs=None, rptrs=None) -> None:
+    def run(k0: int, count: int, ptrs=None) -> None:
         ptrs = ptrs or [base + (k % copies) * stride for k in range(k0, k0 + count)]
-        if split:
-            rptrs = rptrs or [rbase + (k % copies) * rstride for k in range(k0, k0 + count)]
-            worker.process_split_batches_emit(rptrs, ptrs, desc, verdict, hdr, n, sh)
-        elif mode == "emit":
+        if mode == "emit":
             worker.process_batches_emit(ptrs, desc, verdict, hdr, n, sh)
         else:
             worker.process_batches(ptrs, desc, verdict, n, sh)
 
     timed = gpu.GpuWorker.frames_list([base + (k % copies) * stride
                                        for k in range(warmup, warmup + steps)])
-    rtimed = (gpu.GpuWorker.frames_list([rbase + (k % copies) * rstride
-                                         for k in range(warmup, warmup + steps)])
-              if split else None)
     run(0, warmup)
     torch.cuda.synchronize(dev)
     worker.timing_span(EVENT_EVERY, EVENT_SPAN)
@@ -418,7 +402,7 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run(warmup, steps, timed, rtimed)
+    run(warmup, steps, timed)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -429,9 +413,7 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     cms += gms
     worker.close()
     del pool, desc, verdict, hdr
-    if split:
-        del rpool
-    bpp = algorithmic_bytes(wl, v, emit=mode == "emit" or split)
+    bpp = algorithmic_bytes(wl, v, emit=mode == "emit")
     kern_s = cms / launches / 1e3 if launches else float("nan")
     achieved = float(bpp.sum()) / kern_s / 1e9
     return {"workload": WORKLOADS["C"], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
@@ -441,10 +423,8 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "kernel_ms": round(kern_s * 1e3, 5),
                          "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
-                         "traffic": None if split else pmc_traffic("C", n, mode)},
-            "format": ("header-split: each packet's first 64 bytes in a dense row beside the "
-                       "full frames (upe_gpu_process_split_emit)") if split else
-                      "packed frames (upe_gpu_process_emit)",
+                         "traffic": pmc_traffic("C", n, mode)},
+            "format": "packed frames (upe_gpu_process_emit)",
             "what": f"all ranks at once after the main region, {copies} distinct batch copies "
                     "cycled, same timing protocol as value (barrier, max over ranks)"}
 
@@ -467,11 +447,13 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
     """BASELINE configs[3] (16M packets: IPv4 options, TCP data offsets, 10 % malformed, v4 / v6
     mixed per wave; 64k rules, the tuple-space index) timed after the main region with the same
     protocol (emit mode, distinct batch copies cycled, wall time over `steps` launches; HIP
-    events around every launch split classify and the rule_stats group-by).  Its roofline is
-    the VALU issue rate (the rule work, not bytes, was expected to bound it): the
-    classify kernel's VALU wave-instructions per launch (committed PMC, tools/pmc_valu.py) over
-    the live classify time, against 1024 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz; the
-    HBM fractions follow.  Not `value`."""
+    events around every launch split classify and the rule_stats group-by).  Two rooflines for
+    the classify kernel, both from committed PMC passes over the live classify time: the VALU
+    issue rate (SURVEY.md §8(d) expected the rule work to bound it; SQ_INSTS_VALU per launch,
+    tools/pmc_valu.py, against 1024 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz) and the
+    bytes requested past L2 (2 x FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.py) against HBM;
+    `bound` names the one nearer its peak (measured round 4: the bytes, ~0.8 of 8 TB/s, VALU
+    ~0.33).  The algorithmic-bytes fraction follows.  Not `value`."""
     from upe_amd import gpu, synth
 
     t_gen = time.perf_counter()
@@ -513,32 +495,41 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
     bpp = algorithmic_bytes(wl, v, emit=True)
     traffic = pmc_traffic("D", n, "emit")
     pv = pmc_valu("D", n, "emit")
-    roof = {"bound": "valu", "unit": "G VALU wave-instructions/s", "peak": round(VALU_PEAK_G, 1),
-            "kernel": "upe_classify (tuple-space variant)", "classify_ms": round(classify_s * 1e3, 4),
+    roof = {"kernel": "upe_classify (tuple-space variant)", "classify_ms": round(classify_s * 1e3, 4),
             "group_by_ms": round(gms / launches, 4), "event_samples": int(launches)}
+    valu = {"unit": "G VALU wave-instructions/s", "peak": round(VALU_PEAK_G, 1)}
     if pv:
         ach = pv["sq_insts_valu"] / classify_s / 1e9
-        roof.update({"achieved": round(ach, 1), "frac": round(ach / VALU_PEAK_G, 4),
+        valu.update({"achieved": round(ach, 1), "frac": round(ach / VALU_PEAK_G, 4),
                      "valu_insts_per_launch": pv["sq_insts_valu"],
                      "frac_pmc_cycles": round(pv["valu_frac"], 4),
-                     "valu_lane_insts_per_packet": round(pv["valu_insts_per_packet"], 1),
-                     "source": "VALU instructions: profiles/pmc_configD_emit_valu.json (rocprofv3 "
-                               "SQ_INSTS_VALU per classify launch); time: this run's HIP events; "
-                               "frac_pmc_cycles: the PMC run's own GRBM_GUI_ACTIVE cycles"})
+                     "valu_wave_insts_per_64_packets": round(pv["valu_insts_per_packet"], 1),
+                     "source": "profiles/pmc_configD_emit_valu.json (rocprofv3 SQ_INSTS_VALU per "
+                               "classify launch) / this run's classify time (HIP events); "
+                               "frac_pmc_cycles: over the PMC run's own GRBM_GUI_ACTIVE cycles"})
     else:
-        roof.update({"achieved": None, "frac": None,
+        valu.update({"achieved": None, "frac": None,
                      "source": "no committed VALU PMC summary for this batch size"})
     hbm_alg = float(bpp.sum()) / step_s / 1e9
-    roof["hbm"] = {"achieved": round(hbm_alg, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                   "frac": round(hbm_alg / HBM_PEAK_GBPS, 4),
-                   "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
-                   "basis": "algorithmic bytes per step / step kernel time (classify + group-by)"}
+    hbm = {"unit": "GB/s", "peak": HBM_PEAK_GBPS, "traffic": traffic,
+           "algorithmic": {"achieved": round(hbm_alg, 1), "frac": round(hbm_alg / HBM_PEAK_GBPS, 4),
+                           "bytes_per_packet": round(float(bpp.sum()) / n, 2),
+                           "basis": "algorithmic bytes per step / step kernel time (classify + group-by)"}}
     if traffic:
-        roof["hbm"]["traffic"] = traffic
-        roof["hbm"]["traffic_frac"] = round(traffic / classify_s / 1e9 / HBM_PEAK_GBPS, 4)
-        roof["hbm"]["traffic_note"] = ("bytes requested past L2 per classify launch (PMC, "
-                                       "profiles/pmc_configD_emit.json; Infinity-Cache hits "
-                                       "included) / classify time")
+        t_ach = traffic / classify_s / 1e9
+        hbm.update({"achieved": round(t_ach, 1), "frac": round(t_ach / HBM_PEAK_GBPS, 4),
+                    "source": "bytes requested past L2 per classify launch (PMC, "
+                              "profiles/pmc_configD_emit.json: 2 x FETCH_SIZE + WRITE_SIZE; "
+                              "Infinity-Cache hits included, so an upper bound on HBM bytes) / "
+                              "this run's classify time"})
+    else:
+        hbm.update({"achieved": None, "frac": None})
+    roof["valu"] = valu
+    roof["hbm"] = hbm
+    fv, fh = valu.get("frac") or 0.0, hbm.get("frac") or 0.0
+    top = hbm if fh >= fv else valu
+    roof.update({"bound": "hbm" if top is hbm else "valu", "achieved": top.get("achieved"),
+                 "peak": top["peak"], "unit": top["unit"], "frac": top.get("frac")})
     return {"workload": WORKLOADS["D"] + f", {n} packets per step", "value": round(n * steps / elapsed / 1e6, 2),
             "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps,
             "rule_index": "tuple space" if kind == 1 else "linear scan",
@@ -647,9 +638,6 @@ def main() -> None:
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
     ap.add_argument("--imix-copies", type=int, default=32)
-    ap.add_argument("--imix-split", type=int, default=1,
-                    help="1: also time the IMIX leg as header-split batches "
-                         "(upe_gpu_process_split_emit), reported as \"imix_split\"")
     ap.add_argument("--config-d-steps", type=int, default=20,
                     help="timed steps of the config D leg (16M packets, 64k rules; N=1 config B "
                          "runs; 0 skips it)")
@@ -796,13 +784,10 @@ def main() -> None:
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
                                     args.workers_per_gpu, args.steps)
-    imix = imix_split = None
+    imix = None
     if args.config == "B" and not args.no_imix and not args.packets:
         imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
                         args.imix_copies)
-        if args.mode == "emit" and args.imix_split:
-            imix_split = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup,
-                                  args.mode, args.imix_copies, split=True)
     ring = None
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
@@ -912,8 +897,6 @@ def main() -> None:
             out["other_mode"] = other
         if imix:
             out["imix"] = imix
-        if imix_split:
-            out["imix_split"] = imix_split
         if ring:
             out["ring"] = ring
         if dleg:

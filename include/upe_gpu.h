@@ -268,25 +268,6 @@ typedef struct {
 int upe_gpu_process_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
                          uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n, void *stream);
 
-/* A header-split batch in emit mode (the layout a NIC's header-data split produces): d_hdrs
- * holds each packet's first 64 bytes as one dense 64-byte row (row i = bytes 0..63 of packet i,
- * zero past its len; 16-byte aligned), d_frames / d_desc the full frames as for
- * upe_gpu_process_emit().  The kernel reads bytes 0..63 from the rows — whole lines, coalesced
- * across each wave, instead of a window scattered over the frame span — and bytes 64.. from the
- * frame only for frames that have them.  Verdicts, records, counters, rule_stats and the L1 state
- * equal upe_gpu_process_emit() on the same frames (an answered ARP request is rewritten in its
- * frame, as there).  0 / -1. */
-int upe_gpu_process_split_emit(upe_gpu_ctx_t *ctx, const uint8_t *d_hdrs, uint8_t *d_frames,
-                               const uint64_t *d_desc, uint32_t *d_verdict, upe_hdr_rec_t *d_hdr,
-                               size_t n, void *stream);
-/* `count` header-split batches back to back from native code (batch k: d_hdrs_list[k] and
- * d_frames_list[k], host arrays of device pointers, sharing d_desc, d_verdict and d_hdr), as
- * upe_gpu_process_batches_emit() does for ordinary batches. */
-int upe_gpu_process_split_batches_emit(upe_gpu_ctx_t *ctx, const uint8_t *const *d_hdrs_list,
-                                       uint8_t *const *d_frames_list, const uint64_t *d_desc,
-                                       uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, size_t n,
-                                       size_t count, void *stream);
-
 /* A ring of `count` resident batches of n packets each in ONE launch (throughput mode): the
  * batches lie back to back in the "Batch layout" (batch j = descriptors, verdicts and records
  * [j*n, (j+1)*n), frames anywhere in d_frames) and are classified in ring order by one
@@ -530,8 +511,7 @@ int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
  * defers them, and the launch's last workgroup answers them. */
 typedef struct {
     uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back,
-                          4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host),
-                          6 a header-split batch */
+                          4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host) */
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */

@@ -3,10 +3,9 @@ timed like bench.py (emit mode, distinct batch copies cycled, HIP events around 
 
   packed       upe_gpu_process_emit from a calloc'd worker (the NDP entry :: -> 00:..:00 does
                not agree with the NDP table, so the decoupled look-back stays live)
-  split        upe_gpu_process_split_emit (header rows beside the frames), same state
   agree        packed, but the L1 entries set to entries the tables hold (upe_gpu_set_l1): the
                launches switch to the kernel without look-back
-  agree_split  both
+(round 4 also measured header-split batches, since removed: profiles/pmc_configC_limiter.json)
 
 With UPE_GPU_LIB_DIAG=<ablation build> the same runs time a kernel with parts removed (results
 wrong by design).  Usage: python tools/c_probe.py <setting> [launches] > json line."""
@@ -30,7 +29,6 @@ def main() -> None:
 
     setting = sys.argv[1] if len(sys.argv) > 1 else "packed"
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    split = "split" in setting
     wl = synth.config_c()
     n = wl.n
     dev = torch.device("cuda", 0)
@@ -41,15 +39,6 @@ def main() -> None:
     for c in range(copies):
         pool_f[c * fb: c * fb + wl.frames.nbytes].copy_(fr)
     del fr
-    rb = 0
-    if split:
-        rows = synth.header_rows(wl)
-        rb = rows.nbytes
-        rw = torch.from_numpy(rows.reshape(-1)).to(dev)
-        pool_r = torch.empty(copies * rb, dtype=torch.uint8, device=dev)
-        for c in range(copies):
-            pool_r[c * rb: (c + 1) * rb].copy_(rw)
-        del rw
     desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
@@ -66,15 +55,11 @@ def main() -> None:
         w.set_l1(l1)
     sh = torch.cuda.current_stream(dev).cuda_stream
     bf = pool_f.data_ptr()
-    br = pool_r.data_ptr() if split else 0
 
     def run(k0: int, count: int) -> None:
         for k in range(k0, k0 + count):
             c = k % copies
-            if split:
-                w.process_split_emit(br + c * rb, bf + c * fb, desc, verdict, hdr, n, sh)
-            else:
-                w.process_emit(bf + c * fb, desc, verdict, hdr, n, sh)
+            w.process_emit(bf + c * fb, desc, verdict, hdr, n, sh)
 
     run(0, 20)
     torch.cuda.synchronize(dev)

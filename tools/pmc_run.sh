@@ -22,5 +22,5 @@ for g in $groups; do
     rdreq) ctr="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" ;;
     dram) ctr="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum" ;;
   esac
-  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${cfg}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_${mode}_$g.log 2>&1 || echo "pass $g failed rc=$?"
+  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${cfg}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_${mode}_$g.log 2>&1 || { echo "pass $g failed rc=$?"; exit 1; }
 done

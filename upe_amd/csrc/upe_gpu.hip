@@ -322,9 +322,6 @@ struct Args {
     uint32_t* ring_wg;
     unsigned long long* ring_done;
     unsigned long long* ring_t0;
-    // header-split batch (upe_gpu_process_split_emit): bytes 0..63 of packet i at slab[4 i ..
-    // 4 i + 3] (zero past len); bytes 64.. from the frame.  nullptr: every byte from the frame.
-    const uint4* slab;
 };
 // Batch k's state slots, from Args (DevState comment).
 __device__ __forceinline__ const DevL1* l1_in(const Args& a) { return &a.st->l1[a.k6 % 2].s; }
@@ -1176,7 +1173,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kHost = false, bool kSplit = false>
+          bool kHost = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1213,34 +1210,30 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // ---- header window: bytes 0..79 as 16-byte loads issued together.  Chunks at or past len
     // are not loaded (they read as zero, as in a zero-filled pktbuf): a 64-byte frame costs
     // four loads, not five.  Frames shorter than 49 bytes never take the fast path.
-    // (A header-split batch, a.slab: bytes 0..63 as one dense 64-byte row per packet — whole
-    // lines, coalesced across the wave — and bytes 64..79 from the frame when it has them.)
-    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[24], uint32_t pi) {
+    auto load_window = [&](uint64_t dsc, bool live, uint32_t (&w)[24]) {
 #pragma unroll
         for (int j = 0; j < 24; ++j) w[j] = 0;
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            const uint4* h = kSplit ? a.slab + 4 * (size_t)pi : q;
 #pragma unroll
             for (int c = 0; c < 5; ++c) {
                 if (c < 3 || len > 16u * c) {
-                    const uint4 v = c < 4 ? h[c] : q[c];
+                    const uint4 v = q[c];
                     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
                 }
             }
         }
     };
     struct Win { uint4 c0, c1, c2, c3, c4; };
-    auto fetch_window = [&](uint64_t dsc, bool live, uint32_t pi) -> Win {
+    auto fetch_window = [&](uint64_t dsc, bool live) -> Win {
         const uint4 z = make_uint4(0, 0, 0, 0);
         Win v{z, z, z, z, z};
         if (live) {
             const uint32_t len = (uint32_t)(dsc & 0xFFFFu);
             const uint4* q = reinterpret_cast<const uint4*>(a.frames + ((size_t)(dsc >> 20) << 4));
-            const uint4* h = kSplit ? a.slab + 4 * (size_t)pi : q;
-            v.c0 = h[0]; v.c1 = h[1]; v.c2 = h[2];
-            if (len > 48u) v.c3 = h[3];
+            v.c0 = q[0]; v.c1 = q[1]; v.c2 = q[2];
+            if (len > 48u) v.c3 = q[3];
             if (len > 64u) v.c4 = q[4];
         }
         return v;
@@ -1409,7 +1402,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
             w[20] = w[21] = w[22] = w[23] = 0;
         } else {
-            load_window(dsc, live, w, i);
+            load_window(dsc, live, w);
         }
         have_nw = false;
         dsc_next = 0;
@@ -1540,7 +1533,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // the next chunk's window (its descriptor has been back since early in this chunk):
         // issued here, it arrives while this chunk finishes
         if (kMid && chn != kNone) {
-            nw = fetch_window(dsc_next, chn * 64u + (uint32_t)lane < a.n, chn * 64u + (uint32_t)lane);
+            nw = fetch_window(dsc_next, chn * 64u + (uint32_t)lane < a.n);
             have_nw = true;
         }
 
@@ -2444,26 +2437,21 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 128;
+constexpr int kVarCount = 64;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
-// upe_gpu_process_host; not ring), bit 6 a header-split batch (upe_gpu_process_split_emit; emit
-// only, not ring or host).
-enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
-       VAR_SPLIT = 64 };
-int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
-                 bool split = false) {
-    return (split && emit && !ring && !host ? VAR_SPLIT : 0) | (host && !ring ? VAR_HOST : 0) |
-           (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) | (lean ? VAR_LEAN : 0) |
-           (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
+// upe_gpu_process_host; not ring).
+enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32 };
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false) {
+    return (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) |
+           (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
 }
 // The instantiated variants (every combination classify_var can return for a launch).
 constexpr bool var_built(int v) {
     const bool emit = v & VAR_EMIT, lean = v & VAR_LEAN, nolb = v & VAR_NOLB, ring = v & VAR_RING,
-               host = v & VAR_HOST, split = v & VAR_SPLIT;
+               host = v & VAR_HOST;
     if (nolb && !lean) return false;
-    if (ring) return !split && !host && emit && lean && !(v & VAR_TSS);
-    if (split) return emit && !host;
+    if (ring) return !host && emit && lean && !(v & VAR_TSS);
     return true;
 }
 template <int V>
@@ -2471,8 +2459,7 @@ const void* classify_fn_of() {
     if constexpr (var_built(V))
         return reinterpret_cast<const void*>(
             &upe_classify<(V & VAR_TSS) != 0, (V & VAR_EMIT) != 0, (V & VAR_LEAN) != 0,
-                          (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0,
-                          (V & VAR_SPLIT) != 0>);
+                          (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0>);
     else
         return nullptr;
 }
@@ -3257,7 +3244,7 @@ struct RingReq {
 };
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
-                 const RingReq* ring = nullptr, bool host = false, const uint4* slab = nullptr) {
+                 const RingReq* ring = nullptr, bool host = false) {
     if (!c) return fail("null context");
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
@@ -3271,7 +3258,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             const size_t m = n - s0 < kMaxLaunch ? n - s0 : kMaxLaunch;
             if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
                              d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
-                             m, stream, nullptr, host, slab ? slab + 4 * s0 : nullptr) != 0)
+                             m, stream, nullptr, host) != 0)
                 return -1;
         }
         return 0;
@@ -3334,7 +3321,6 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.stats_idx = c->stats_idx;
     a.flow_hash = d_flow_hash;
     a.hdr = reinterpret_cast<uint4*>(d_hdr);
-    a.slab = slab;
     const bool emit = d_hdr != nullptr && n > 0;
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     a.gb = nullptr;
@@ -3390,15 +3376,14 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     // (at most kRingMax batches: one LDS counter each)
     bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, slab != nullptr);
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host,
-                                      slab != nullptr), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3514,29 +3499,6 @@ int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_
                          uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (n && !d_hdr) return fail("null header records");
     return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
-}
-
-int upe_gpu_process_split_emit(upe_gpu_ctx_t* c, const uint8_t* d_hdrs, uint8_t* d_frames,
-                               const uint64_t* d_desc, uint32_t* d_verdict, upe_hdr_rec_t* d_hdr,
-                               size_t n, void* stream) {
-    if (n && !d_hdr) return fail("null header records");
-    if (n && !d_hdrs) return fail("null header rows");
-    if (((uintptr_t)d_hdrs & 15u) != 0) return fail("header rows must be 16-byte aligned");
-    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream, nullptr, false,
-                        reinterpret_cast<const uint4*>(d_hdrs));
-}
-
-int upe_gpu_process_split_batches_emit(upe_gpu_ctx_t* c, const uint8_t* const* d_hdrs_list,
-                                       uint8_t* const* d_frames_list, const uint64_t* d_desc,
-                                       uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n,
-                                       size_t count, void* stream) {
-    if (!c) return fail("null context");
-    if (count && (!d_hdrs_list || !d_frames_list)) return fail("null batch list");
-    for (size_t k = 0; k < count; ++k)
-        if (upe_gpu_process_split_emit(c, d_hdrs_list[k], d_frames_list[k], d_desc, d_verdict,
-                                       d_hdr, n, stream) != 0)
-            return -1;
-    return 0;
 }
 
 int upe_gpu_process_ring_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,

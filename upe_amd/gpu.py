@@ -27,7 +27,6 @@ LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
 VAR_NOLB = 8    # the kernel without look-back
 VAR_RING = 16   # a ring launch whose batches are stamped
 VAR_HOST = 32   # a host path's launch (mapped host memory, host round trip)
-VAR_SPLIT = 64  # a header-split batch
 
 
 # upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
@@ -127,8 +126,6 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_mapped": (I, [P, P, P, P, SZ, P]),
         "upe_gpu_process_mapped_emit": (I, [P, P, P, P, P, SZ, P]),
         "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
-        "upe_gpu_process_split_emit": (I, [P, P, P, P, P, P, SZ, P]),
-        "upe_gpu_process_split_batches_emit": (I, [P, P, P, P, P, P, SZ, SZ, P]),
         "upe_gpu_worker_run": (I, [P, ctypes.POINTER(WorkerOps), P, ctypes.POINTER(WorkerCfg),
                                    P]),
     }
@@ -167,7 +164,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
-            "upe_tx_flush", "upe_gpu_process_split_emit", "upe_gpu_process_split_batches_emit",
+            "upe_tx_flush",
             "upe_gpu_worker_run")
 
 
@@ -300,25 +297,6 @@ class GpuWorker:
         _check(LIB.upe_gpu_process(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
                                    _dev_ptr(verdict), n, stream or None),
                "upe_gpu_process")
-
-    def process_split_emit(self, hdrs, frames, desc, verdict, hdr, n: int, stream=None) -> None:
-        """upe_gpu_process_split_emit: a header-split batch (hdrs: n dense 64-byte rows of the
-        packets' first bytes, device) plus the full frames; emit mode."""
-        _check(LIB.upe_gpu_process_split_emit(self._ctx, _dev_ptr(hdrs), _dev_ptr(frames),
-                                              _dev_ptr(desc), _dev_ptr(verdict), _dev_ptr(hdr),
-                                              n, stream or None),
-               "upe_gpu_process_split_emit")
-
-    def process_split_batches_emit(self, hdrs_list, frames_list, desc, verdict, hdr, n: int,
-                                   stream=None) -> None:
-        """upe_gpu_process_split_batches_emit over native arrays of device pointers (see
-        frames_list())."""
-        hl = hdrs_list if isinstance(hdrs_list, ctypes.Array) else self.frames_list(hdrs_list)
-        fl = frames_list if isinstance(frames_list, ctypes.Array) else self.frames_list(frames_list)
-        _check(LIB.upe_gpu_process_split_batches_emit(self._ctx, hl, fl, _dev_ptr(desc),
-                                                      _dev_ptr(verdict), _dev_ptr(hdr), n, len(fl),
-                                                      stream or None),
-               "upe_gpu_process_split_batches_emit")
 
     def process_mapped(self, frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray,
                        stream=None) -> None:

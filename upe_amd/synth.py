@@ -643,25 +643,6 @@ def header_windows(wl: Workload, window: int = HDR_WINDOW) -> Workload:
                                l1=wl.l1.copy())
 
 
-def header_rows(wl: Workload, row: int = 64) -> np.ndarray:
-    """The header-split side of a batch (upe_gpu_process_split_emit): row i = packet i's first
-    min(len, 64) bytes, zero past len, as a NIC's header-data split lays headers into their own
-    ring.  (n, 64) uint8."""
-    offs = desc_offsets(wl.desc)
-    lens = desc_lens(wl.desc)
-    n = wl.n
-    out = np.zeros((max(n, 1), row), dtype=np.uint8)
-    cols = np.arange(row)
-    chunk = 1 << 16
-    for s in range(0, n, chunk):
-        e = min(n, s + chunk)
-        m = cols[None, :] < np.minimum(lens[s:e], row)[:, None]
-        src = offs[s:e, None] + cols[None, :]
-        blk = out[s:e]
-        blk[m] = wl.frames[src[m]]
-    return out
-
-
 CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d}
 
 
