@@ -170,6 +170,15 @@ def pmc_traffic(config: str, packets: int, mode: str):
     return d["traffic_bytes_per_launch"] if d.get("packets") == packets else None
 
 
+def cpu_quota():
+    """This process's cgroup v2 CPU quota in CPUs (cpu.max), or None when unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        return None
+
+
 def cpu_baseline(wl, threads: int, local: list | None = None, numa_all: bool = True) -> dict:
     """The reference worker timed on this host: one shard and calloc'd worker_t per thread, each
     pinned to its own core — the GPU's NUMA-local cores first (`local`), then the rest of the
@@ -204,13 +213,24 @@ def cpu_baseline(wl, threads: int, local: list | None = None, numa_all: bool = T
             big = synth.config_b(n=1 << 22, seed=2)
             ra = []
             va = oracle.time_reference(big, threads=len(loc), cpus=loc, reps=9, rates=ra)
+            quota = cpu_quota()
             numa = {"value": round(va / 1e6, 3), "unit": "Mpps", "cores": len(loc),
                     "spread": {"min": round(ra[0] / 1e6, 3), "median": round(va / 1e6, 3),
                                "max": round(ra[-1] / 1e6, 3), "passes": len(ra)},
                     "sample": f"{big.n} packets of the same workload (config B, seed 2) split over "
                               "every CPU of the GPU's NUMA node in this process's affinity, one "
-                              "pinned thread each; median of 9 passes after 1 warm-up",
-                    "note": "the node's other jobs share these cores: the spread says how much"}
+                              "pinned thread each; median of 9 passes after 1 warm-up; rate = "
+                              "packets / the slowest thread's time",
+                    "cpu_quota_cpus": quota,
+                    "linear_projection": {"value": round(v1 * len(loc) / 1e6, 3), "unit": "Mpps",
+                                          "what": "single-core rate x NUMA-local cores: the "
+                                                  "node's CPU side if the path scaled perfectly "
+                                                  "(an upper bound, not a measurement)"},
+                    "note": ("this job's cgroup CPU quota (cpu_quota_cpus) is below the thread "
+                             "count, so threads are throttled and the slowest one sets the rate: "
+                             "the measured value is the quota, not the cores — see "
+                             "linear_projection") if quota and quota < len(loc) else
+                            "the node's other jobs share these cores: the spread says how much"}
         return {"value": round(vn / 1e6, 3), "unit": "Mpps", "cores": len(cpus),
                 "numa_local_all": numa,
                 "kind": "reference", "single_core_value": round(v1 / 1e6, 3),
