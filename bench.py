@@ -380,15 +380,17 @@ def host_mapped(worker, wl, reps: int, emit: bool) -> dict:
 
 
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
-             copies_cap: int) -> dict:
+             copies_cap: int, v6_forwarding: bool = False) -> dict:
     """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
     timed the same way as `value`, on every rank at once after the main region, so that a
     multi-GPU run reports the 64 B and the IMIX rates at each N (BASELINE north_star).  Each rank
     takes its own shard (seed 3 + 1000 * rank); `copies_cap` distinct copies of the batch
-    (32 x 373 MB, past the Infinity Cache) are cycled.  Not `value`."""
+    (32 x 373 MB, past the Infinity Cache) are cycled.  Not `value`.  v6_forwarding: the same
+    traffic with the rule table's family-wide wildcards last, so that IPv6 is forwarded through
+    the NDP lookup (config C's seed-3 draw drops all IPv6 at rule 0), reported as `imix_v6fwd`."""
     from upe_amd import gpu, shard, synth
 
-    wl = synth.config_c(seed=3 + 1000 * rank)
+    wl = synth.config_c(seed=3 + 1000 * rank, v6_forwarding=v6_forwarding)
     n = wl.n
     worker = gpu.GpuWorker(local, wl.capacity)
     worker.configure(wl)
@@ -657,6 +659,9 @@ def main() -> None:
     ap.add_argument("--no-imix", action="store_true",
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
+    ap.add_argument("--imix-v6fwd", type=int, default=1,
+                    help="1: also time config C with its family-wide wildcards last (IPv6 "
+                         "forwarded through NDP, deep rule scans), reported as \"imix_v6fwd\"")
     ap.add_argument("--imix-copies", type=int, default=32)
     ap.add_argument("--config-d-steps", type=int, default=20,
                     help="timed steps of the config D leg (16M packets, 64k rules; N=1 config B "
@@ -804,10 +809,13 @@ def main() -> None:
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
                                     args.workers_per_gpu, args.steps)
-    imix = None
+    imix = imix6 = None
     if args.config == "B" and not args.no_imix and not args.packets:
         imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
                         args.imix_copies)
+        if args.imix_v6fwd:
+            imix6 = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
+                             args.imix_copies, v6_forwarding=True)
     ring = None
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
@@ -917,6 +925,9 @@ def main() -> None:
             out["other_mode"] = other
         if imix:
             out["imix"] = imix
+        if imix6:
+            imix6["workload"] = WORKLOADS["C"] + ", family-wide wildcard rules last (IPv6 forwarded)"
+            out["imix_v6fwd"] = imix6
         if ring:
             out["ring"] = ring
         if dleg:

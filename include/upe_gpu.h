@@ -389,6 +389,9 @@ typedef struct {
     uint8_t *pool_base;
     unsigned idle_ns;   /* sleep when the ring is empty and nothing is held (0 = 1000, as
                            src/worker.c:274-277) */
+    size_t pool_bytes;  /* with pool_base: the registered region's size; a frame whose bytes
+                           (at least UPE_FRAME_TAIL of them, what the kernel may read) do not lie
+                           inside it stops the loop with an error instead of reaching the GPU */
 } upe_worker_cfg_t;
 
 /* The GPU-backed replacement of worker_main (reference src/worker.c:255-307), on the calling
@@ -511,7 +514,8 @@ int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
  * defers them, and the launch's last workgroup answers them. */
 typedef struct {
     uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back,
-                          4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host) */
+                          4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host),
+                          6 a linear-scan table past 64 rules (per-family rule lists) */
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */

@@ -310,6 +310,7 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     g.w = w;
     g.device = device;
     g.cfg.pool_base = g_mapped ? (uint8_t *)pool.buffers : NULL;
+    g.cfg.pool_bytes = g_mapped ? pool.capacity * sizeof(pktbuf_t) : 0;
     g.cfg.batch = 65536;
     /* (rule_stats published after every batch, so that the array swapped out at a reload holds
      * exactly the counts up to the swap) */
@@ -531,6 +532,7 @@ int upe_dropin_bench(int gpu, int mapped, int workers, int device, size_t pool_c
             gs[i].w = &ws[i];
             gs[i].device = device;
             gs[i].cfg.pool_base = mapped ? (uint8_t *)pool.buffers : NULL;
+            gs[i].cfg.pool_bytes = mapped ? pool.capacity * sizeof(pktbuf_t) : 0;
             gs[i].cfg.batch = gpu_batch;
             gs[i].stats_every_ns = 100000000ull; /* rule_stats for the stats thread: 10 Hz */
             if (gpu_worker_start(&gs[i], &th[i]) != 0) return -1;

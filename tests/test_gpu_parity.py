@@ -449,3 +449,29 @@ def test_group_by_key_forms(gpu_worker_factory, n_rules, emit):
     assert np.array_equal(stats, r.rule_stats)
     assert counters.tobytes() == r.counters.tobytes()
     assert np.array_equal(frames, r.frames)
+
+
+@pytest.mark.parametrize("emit", [False, True])
+def test_config_c_ipv6_forwarding(gpu_worker_factory, emit):
+    """Config C with its family-wide wildcards moved last (synth.config_c(v6_forwarding=True)):
+    IPv6 packets now reach the NDP lookup and are forwarded with the hop-limit rewrite, and match
+    at spread-out positions of the 1k-rule table (deep linear scans) — against the reference
+    worker itself (oracle/_ref) on the same batch: verdicts, bytes, counters, rule_stats, L1."""
+    from upe_amd.layout import desc_offsets
+
+    wl = synth.config_c(n=60_000, seed=3, v6_forwarding=True)
+    got = _run(gpu_worker_factory, wl, emit=emit)
+    key = ("c6", 60_000)
+    if key not in _D_CACHE:
+        _D_CACHE[key] = oracle.run_reference(wl) if oracle.ref_available() else oracle.run_restated(wl)
+    ref = _D_CACHE[key]
+    frames, verdict, counters, stats, l1 = got
+    assert np.array_equal(verdict, ref.verdict)
+    assert np.array_equal(frames, ref.frames)
+    assert counters.tobytes() == ref.counters.tobytes()
+    assert np.array_equal(stats, ref.rule_stats)
+    assert l1.tobytes() == ref.l1.tobytes()
+    offs = desc_offsets(wl.desc)
+    is6 = wl.frames[offs + 12] == 0x86
+    fwd6 = ((verdict & 0xF) == V_FWD) & is6 & ((verdict & 0x10) != 0)
+    assert fwd6.sum() > 1000, "IPv6 packets must be forwarded through the NDP table"

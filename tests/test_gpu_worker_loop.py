@@ -126,7 +126,8 @@ class Pipeline:
 
     def run(self, w, batch):
         # (PinnedArray memory is mapped for the GPU already: no registration needed)
-        cfg = gpu.WorkerCfg(batch, 32, self.base if self.mapped else None, 0)
+        cfg = gpu.WorkerCfg(batch, 32, self.base if self.mapped else None, 0,
+                            self.pool.array.nbytes if self.mapped else 0)
         counters = np.zeros(1, gpu.COUNTERS_DTYPE)
         rc = gpu.LIB.upe_gpu_worker_run(w._ctx, ctypes.byref(self.ops), None, ctypes.byref(cfg),
                                         counters.ctypes.data)
@@ -235,14 +236,25 @@ def test_worker_loop_argument_checks(gpu_worker_factory):
     w = gpu_worker_factory(wl.capacity)
     try:
         w.configure(wl)
-        bad = gpu.WorkerCfg(0, 65, None, 0)   # bursts above UPE_TX_BATCH_MAX
+        bad = gpu.WorkerCfg(0, 65, None, 0, 0)   # bursts above UPE_TX_BATCH_MAX
         assert gpu.LIB.upe_gpu_worker_run(w._ctx, ctypes.byref(p.ops), None, ctypes.byref(bad),
                                           None) == -1
         assert b"burst" in gpu.LIB.upe_gpu_last_error()
+        # mapped mode: the region's size is required, and a frame outside it never reaches the GPU
+        small = gpu.WorkerCfg(0, 32, p.base, 0, 32)
+        assert gpu.LIB.upe_gpu_worker_run(w._ctx, ctypes.byref(p.ops), None, ctypes.byref(small),
+                                          None) == -1
+        assert b"pool_bytes" in gpu.LIB.upe_gpu_last_error()
+        short = gpu.WorkerCfg(0, 32, p.base, 0, 4 * STRIDE)   # the 5th frame lies past the end
+        assert gpu.LIB.upe_gpu_worker_run(w._ctx, ctypes.byref(p.ops), None, ctypes.byref(short),
+                                          None) == -1
+        assert b"inside the registered pool" in gpu.LIB.upe_gpu_last_error()
+        assert sorted(p.freed) == list(range(len(p.freed))) and len(p.freed) == sum(p.pops)
         ops = gpu.WorkerOps.from_buffer_copy(p.ops)
         ops.tx_send_batch = gpu.TX_BATCH_FN()
+        pops = len(p.pops)
         assert gpu.LIB.upe_gpu_worker_run(w._ctx, ctypes.byref(ops), None, None, None) == -1
-        assert not p.pops, "nothing may be popped when the call is refused"
+        assert len(p.pops) == pops, "nothing may be popped when the call is refused"
     finally:
         w.close()
         p.pool.free()

@@ -10,7 +10,7 @@ for r in $(seq 1 $rounds); do
     envs=""; [ "$lib" != "product" ] && envs="UPE_GPU_LIB_DIAG=$lib"
     f=gpurun_out/ab/${label}_$r.json
     timeout -k 10 180 env $envs python bench.py --no-cpu-baseline --no-hbm-probe \
-        --ring 0 --host-reps 0 --no-host-emit --no-host-mapped > $f 2> ${f%.json}.err
+        --ring 0 --host-reps 0 --no-host-emit --no-host-mapped --imix-v6fwd 0 > $f 2> ${f%.json}.err
     rc=$?
     python - "$label" "$f" "$rc" <<'PY'
 import json, sys

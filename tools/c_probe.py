@@ -5,6 +5,8 @@ timed like bench.py (emit mode, distinct batch copies cycled, HIP events around 
                not agree with the NDP table, so the decoupled look-back stays live)
   agree        packed, but the L1 entries set to entries the tables hold (upe_gpu_set_l1): the
                launches switch to the kernel without look-back
+  c6           packed, config C with its family-wide wildcards last (synth.config_c
+               v6_forwarding=True): IPv6 forwarded through NDP, deep rule scans
 (round 4 also measured header-split batches, since removed: profiles/pmc_configC_limiter.json)
 
 With UPE_GPU_LIB_DIAG=<ablation build> the same runs time a kernel with parts removed (results
@@ -29,7 +31,7 @@ def main() -> None:
 
     setting = sys.argv[1] if len(sys.argv) > 1 else "packed"
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    wl = synth.config_c()
+    wl = synth.config_c(v6_forwarding=setting == "c6")
     n = wl.n
     dev = torch.device("cuda", 0)
     copies = 24

@@ -154,6 +154,19 @@ constexpr uint32_t kRuleV6Words = 0x80000000u;
 struct __attribute__((aligned(16))) RuleV6 {
     uint32_t s[3], sm[3], d[3], dm[3], pad[4];
 };
+// FamTable (linear-scan tables past the LDS size): the rules an IPv4 key can match (ip_ver 4 or
+// 0) and those an IPv6 key can match (6 or 0), each list in priority order, so that a lane walks
+// only its own family's list — a wave's scan lasts as long as its deepest lane's position in its
+// family's list, not in the whole table.  Image: fam4 RuleV4, then fam6 (RuleV4, RuleV6) pairs,
+// then the lists' sorted indexes (u32, fam4 then fam6); padding entries never match.  An IPv6
+// entry is 80 bytes: the RuleV4 words, then RuleV6's s[3] sm[3] d[3] dm[3].  When the IPv6 list
+// fits beside the launch's other LDS data it is staged there (Args::fam6_lds): an IPv6 lane's
+// scan, the deep one in mixed tables, then reads LDS instead of the scalar cache.
+constexpr uint32_t kFamV6Stride = 5;   // uint4 per IPv6 entry
+#ifndef UPE_FAM_LDS
+#define UPE_FAM_LDS 1
+#endif
+constexpr bool kFamLds = UPE_FAM_LDS;
 
 // L1 state in word form + whether each entry agrees with the current neighbour snapshot.
 // DevState keeps two, by batch parity (see "Sequential state between batches").
@@ -280,6 +293,10 @@ struct Args {
     const RuleV6* rv6;
     const int2* rinfo;
     uint32_t nrules_pad;           // multiple of kUnroll, padding rules never match
+    // per-family rule lists of a linear-scan table past the LDS size (FamTable comment)
+    const uint4* fam;
+    uint32_t fam4, fam6;           // entries per list, multiples of kUnroll
+    uint32_t fam6_lds;             // the IPv6 list is staged in LDS (after the neighbour indexes)
     uint32_t port_mac_lo, port_mac_hi, port_ip4;
     NeighIndex arp, ndp;
     DevState* st;
@@ -662,6 +679,89 @@ __device__ __forceinline__ uint32_t scan_rules(const Args& a, bool done, bool is
         if (__all(done)) break;
     }
     return hit;
+}
+
+// First match over the per-family lists (FamTable): the same rule tests as scan_rules, each lane
+// against its own family's list; `pos` is the lane's position in its list, turned into the
+// sorted index after the loop (reference src/rule_table.c:163-176: the first match in (priority,
+// rule_id) order — a rule of the other family cannot match, so it is skipped, not reordered).
+template <bool V6>
+__device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6, uint32_t k0,
+                                             uint32_t k1, const uint32_t s[4], const uint32_t d[4],
+                                             uint32_t& act, const uint4* l6) {
+    // the IPv4 lanes' list, then the IPv6 lanes' list (one loop after the other: interleaving
+    // both in one loop held twice the rule words in SGPRs and spilled)
+    const auto* f4 = as_const<u32x8>(a.fam);
+    const uint4* f6 = a.fam + 2 * (size_t)a.fam4;
+    uint32_t pos = kNone;
+    bool dn = done || is6;
+    for (uint32_t b = 0; b < a.fam4; b += kUnroll) {
+        if (!__any(!dn)) break;
+        const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const u32x8 r = f4[base + u];
+            const uint32_t x = ((k0 ^ r[0]) & r[1]) | ((k1 ^ r[2]) & r[3]) |
+                               ((s[0] ^ r[4]) & r[5]) | ((d[0] ^ r[6]) & r[7]);
+            if (!dn && x == 0) {
+                pos = base + u;
+                act = r[2];
+                dn = true;
+            }
+        }
+    }
+    if (V6 && a.fam6_lds) {
+        dn = done || !is6;
+        for (uint32_t b = 0; b < a.fam6; b += kUnroll) {
+            if (!__any(!dn)) break;
+            const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint4* e = l6 + kFamV6Stride * (base + u);
+                const uint4 e0 = e[0], e1 = e[1];
+                uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                             ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
+                if (__builtin_amdgcn_readfirstlane(e0.w) & kRuleV6Words) {
+                    const uint4 e2 = e[2], e3 = e[3], e4 = e[4];
+                    // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3
+                    x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+                         ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+                }
+                if (!dn && x == 0) {
+                    pos = base + u;
+                    act = e0.z;
+                    dn = true;
+                }
+            }
+        }
+    } else if (V6) {
+        // (two entries per step: four held 96 rule words in SGPRs and spilled)
+        dn = done || !is6;
+        for (uint32_t b = 0; b < a.fam6; b += 2) {
+            if (!__any(!dn)) break;
+            const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint4* e = f6 + (size_t)kFamV6Stride * (base + u);
+                const u32x8 r = *as_const<u32x8>(e);
+                uint32_t x = ((k0 ^ r[0]) & r[1]) | ((k1 ^ r[2]) & r[3]) |
+                             ((s[0] ^ r[4]) & r[5]) | ((d[0] ^ r[6]) & r[7]);
+                if (__builtin_amdgcn_readfirstlane(r[3]) & kRuleV6Words) {
+                    const u32x16 q = *as_const<u32x16>(e + 2);
+                    x |= ((s[1] ^ q[0]) & q[3]) | ((s[2] ^ q[1]) & q[4]) | ((s[3] ^ q[2]) & q[5]) |
+                         ((d[1] ^ q[6]) & q[9]) | ((d[2] ^ q[7]) & q[10]) | ((d[3] ^ q[8]) & q[11]);
+                }
+                if (!dn && x == 0) {
+                    pos = base + u;
+                    act = r[2];
+                    dn = true;
+                }
+            }
+        }
+    }
+    if (pos == kNone) return kNone;
+    const uint32_t* idx = reinterpret_cast<const uint32_t*>(f6 + (size_t)kFamV6Stride * a.fam6);
+    return idx[(is6 ? a.fam4 : 0u) + pos];
 }
 
 // Key hash of the tuple-space index (host and device agree bit for bit).
@@ -1173,7 +1273,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kHost = false>
+          bool kHost = false, bool kFam = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1196,7 +1296,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const bool lds_stats = a.nrules_pad <= (uint32_t)kLdsStatsMax;
-    const bool small_stats = a.nrules_pad <= (uint32_t)kSmallRules;
+    // (kFam: a linear-scan table past kSmallRules, scanned through its family lists; the host
+    // picks the instantiation, so the small-table kernels carry no FamTable code)
+    const bool small_stats = !kFam && a.nrules_pad <= (uint32_t)kSmallRules;
 
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
@@ -1293,6 +1395,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     uint4* s_fp4 = s_ndp + 2 * a.ndp_lds;
     if (kTssMode)
         for (uint32_t k = tid; k < a.fp_lds; k += kBlock) s_fp4[k] = a.tfs[k];
+    // linear-scan tables past kSmallRules: the IPv6 family list, when the host found room
+    const uint4* s_fam6 = s_fp4;
+    if (kFam && a.fam6_lds) {
+        const uint4* g = a.fam + 2 * (size_t)a.fam4;
+        for (uint32_t k = tid; k < kFamV6Stride * a.fam6; k += kBlock) s_fp4[k] = g[k];
+    }
     const uint16_t* s_fps = kTssMode && a.fp_lds ? reinterpret_cast<const uint16_t*>(s_fp4) : nullptr;
     __syncthreads();
     STAMP(1);
@@ -1503,12 +1611,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else {
             // small tables from their LDS copy, larger ones through the scalar unit
             const uint32_t nr = a.nrules_pad;
-            if (small_stats)
+            if (!kFam)
                 ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
                              : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
             else
-                ri = need_v6 ? scan_rules<true, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
-                             : scan_rules<false, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
+                ri = need_v6 ? scan_fam<true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6)
+                             : scan_fam<false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6);
         }
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
@@ -2193,6 +2301,9 @@ struct upe_gpu_ctx {
     RuleV4* rv4 = nullptr;
     RuleV6* rv6 = nullptr;
     int2* rinfo = nullptr;
+    uint4* fam = nullptr;                      // FamTable image (linear-scan tables > kSmallRules)
+    size_t fam_alloc = 0;                      // bytes
+    uint32_t fam4 = 0, fam6 = 0;
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
@@ -2437,20 +2548,25 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 64;
+constexpr int kVarCount = 128;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
-// upe_gpu_process_host; not ring).
-enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32 };
-int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false) {
-    return (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) |
-           (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
+// upe_gpu_process_host; not ring), bit 6 a linear-scan table past kSmallRules (FamTable; not
+// tuple space).
+enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
+       VAR_FAM = 64 };
+int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
+                 bool fam = false) {
+    return (fam && !tss ? VAR_FAM : 0) | (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) |
+           (lean && nolb ? VAR_NOLB : 0) | (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) |
+           (emit ? VAR_EMIT : 0);
 }
 // The instantiated variants (every combination classify_var can return for a launch).
 constexpr bool var_built(int v) {
     const bool emit = v & VAR_EMIT, lean = v & VAR_LEAN, nolb = v & VAR_NOLB, ring = v & VAR_RING,
                host = v & VAR_HOST;
     if (nolb && !lean) return false;
+    if ((v & VAR_FAM) && (v & VAR_TSS)) return false;
     if (ring) return !host && emit && lean && !(v & VAR_TSS);
     return true;
 }
@@ -2459,7 +2575,8 @@ const void* classify_fn_of() {
     if constexpr (var_built(V))
         return reinterpret_cast<const void*>(
             &upe_classify<(V & VAR_TSS) != 0, (V & VAR_EMIT) != 0, (V & VAR_LEAN) != 0,
-                          (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0>);
+                          (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0,
+                          (V & VAR_FAM) != 0>);
     else
         return nullptr;
 }
@@ -2721,7 +2838,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->gb, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs,
+                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs, c->fam,
                     c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
                     c->hist_part};
@@ -3008,6 +3125,52 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     HIP_TRY(hipMemcpy(c->rv4, v4.data(), pad * sizeof(RuleV4), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->rv6, v6.data(), pad * sizeof(RuleV6), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->rinfo, info.data(), pad * sizeof(int2), hipMemcpyHostToDevice));
+    // linear-scan tables past the LDS copy: the per-family lists (FamTable)
+    c->fam4 = c->fam6 = 0;
+    if (pad > (size_t)kSmallRules) {
+        std::vector<uint32_t> l4, l6;
+        for (size_t i = 0; i < count; ++i) {
+            const uint8_t ver = rules[i].ip_ver;
+            if (ver == 0 || ver == 4) l4.push_back((uint32_t)i);
+            if (ver == 0 || ver == 6) l6.push_back((uint32_t)i);
+        }
+        const size_t n4 = (l4.size() + kUnroll - 1) / kUnroll * kUnroll;
+        const size_t n6 = (l6.size() + kUnroll - 1) / kUnroll * kUnroll;
+        // (+1: the scalar scan loads an IPv6 entry's last 48 bytes as 64)
+        std::vector<uint4> img(2 * n4 + kFamV6Stride * n6 + (n4 + n6 + 3) / 4 + 1);
+        memset(img.data(), 0, img.size() * sizeof(uint4));
+        RuleV4 never;
+        memset(&never, 0, sizeof never);
+        never.x0 = 0xFF;   // ip_ver byte 0xFF against a key version of 4 or 6
+        never.m0 = 0xFF;
+        uint32_t* idx = reinterpret_cast<uint32_t*>(img.data() + 2 * n4 + kFamV6Stride * n6);
+        for (size_t j = 0; j < n4; ++j) {
+            const RuleV4& e = j < l4.size() ? v4[l4[j]] : never;
+            memcpy(&img[2 * j], &e, sizeof e);
+            idx[j] = j < l4.size() ? l4[j] : 0u;
+        }
+        for (size_t j = 0; j < n6; ++j) {
+            uint4* o = &img[2 * n4 + kFamV6Stride * j];
+            if (j < l6.size()) {
+                memcpy(o, &v4[l6[j]], sizeof(RuleV4));
+                memcpy(o + 2, &v6[l6[j]], 3 * sizeof(uint4));   // s, sm, d, dm (12 words)
+            } else {
+                memcpy(o, &never, sizeof never);
+            }
+            idx[n4 + j] = j < l6.size() ? l6[j] : 0u;
+        }
+        const size_t bytes = img.size() * sizeof(uint4);
+        if (bytes > c->fam_alloc) {
+            if (c->fam) (void)hipFree(c->fam);
+            c->fam = nullptr;
+            c->fam_alloc = 0;
+            HIP_TRY(hipMalloc(&c->fam, bytes));
+            c->fam_alloc = bytes;
+        }
+        HIP_TRY(hipMemcpy(c->fam, img.data(), bytes, hipMemcpyHostToDevice));
+        c->fam4 = (uint32_t)n4;
+        c->fam6 = (uint32_t)n6;
+    }
     c->nrules = (uint32_t)count;
     c->nrules_pad = (uint32_t)pad;
     c->rinfo_host = info;
@@ -3292,6 +3455,9 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.n = (uint32_t)n;
     a.rv4 = c->rv4;
     a.rv6 = c->rv6;
+    a.fam = c->fam;
+    a.fam4 = c->fam4;
+    a.fam6 = c->fam6;
     a.rinfo = c->rinfo;
     a.nrules_pad = c->nrules_pad;
     a.arp = arp_index(c);
@@ -3356,6 +3522,11 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         a.fp_lds = c->nfs;
         lds += c->nfs * sizeof(uint4);
     }
+    a.fam6_lds = 0u;
+    if (kFamLds && !c->tss && c->fam6 && lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
+        a.fam6_lds = 1u;
+        lds += kFamV6Stride * c->fam6 * sizeof(uint4);
+    }
     // the lean emit kernel when nothing it leaves out is needed (non-empty neighbour indexes
     // all in LDS, no flow_hash, no length side array)
     const bool lean = !d_flow_hash && (c->tss || !a.gb) &&
@@ -3376,14 +3547,15 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     // (at most kRingMax batches: one LDS counter each)
     bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host);
+    const bool fam = !c->tss && c->nrules_pad > (uint32_t)kSmallRules;
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, fam);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host, fam), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3400,7 +3572,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         const size_t tpb = (ring->per / 64) / tw;
         if (stamp && (tpb < grid || tpb % grid != 0)) stamp = false;
         if (!stamp) {
-            var = classify_var(c->tss, emit, lean, c->no_lb, false);
+            var = classify_var(c->tss, emit, lean, c->no_lb, false, false, fam);
             if (resident_grid(c, var, lds, s) == 0) return -1;
         } else {
             const size_t nb = n / ring->per;

@@ -44,6 +44,7 @@ typedef struct {
     size_t cap;        /* packets per batch */
     unsigned burst;
     uint8_t *pool;     /* mapped mode: registered region the frames lie in */
+    size_t pool_bytes;
     /* the batch being gathered: handles in arrival order, and the pinned arrays the GPU reads */
     void **bufs;
     size_t n;
@@ -199,11 +200,14 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
     L.cap = cfg && cfg->batch ? cfg->batch : 65536;
     L.burst = cfg && cfg->burst ? cfg->burst : 32;
     L.pool = cfg ? cfg->pool_base : NULL;
+    L.pool_bytes = cfg ? cfg->pool_bytes : 0;
     const long idle = cfg && cfg->idle_ns ? (long)cfg->idle_ns : 1000;
     if (L.burst > UPE_TX_BATCH_MAX) return upe_gpu_set_last_error("burst exceeds UPE_TX_BATCH_MAX");
     if (L.cap > ((size_t)1 << 24)) return upe_gpu_set_last_error("batch exceeds 2^24 packets");
     if (L.pool && ((uintptr_t)L.pool & 15u))
         return upe_gpu_set_last_error("pool_base must be 16-byte aligned");
+    if (L.pool && L.pool_bytes < UPE_FRAME_TAIL)
+        return upe_gpu_set_last_error("pool_bytes must give the registered region's size");
     L.bufs = malloc((L.cap + L.burst) * sizeof(void *));
     L.bq_cap = L.cap + 2;
     L.bq = malloc(L.bq_cap * sizeof(unsigned));
@@ -247,8 +251,11 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
             const size_t len = ops->len(user, b);
             if (L.pool) {
                 const size_t off = (size_t)(d - L.pool);
-                if ((off & 15u) || len > 0xFFFFu) {
-                    upe_gpu_set_last_error("a frame is not 16-byte aligned in the pool");
+                const size_t span = len > UPE_FRAME_TAIL ? len : UPE_FRAME_TAIL;
+                if (d < L.pool || off > L.pool_bytes || span > L.pool_bytes - off || (off & 15u) ||
+                    len > 0xFFFFu) {
+                    upe_gpu_set_last_error(
+                        "a frame is not 16-byte aligned inside the registered pool");
                     for (unsigned r = j; r < k; r++) L.bufs[L.n++] = burst[r];
                     goto fail;
                 }

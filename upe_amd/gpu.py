@@ -27,6 +27,7 @@ LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
 VAR_NOLB = 8    # the kernel without look-back
 VAR_RING = 16   # a ring launch whose batches are stamped
 VAR_HOST = 32   # a host path's launch (mapped host memory, host round trip)
+VAR_FAM = 64    # a linear-scan table past 64 rules, scanned through per-family rule lists
 
 
 # upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
@@ -62,7 +63,7 @@ class WorkerOps(ctypes.Structure):
 class WorkerCfg(ctypes.Structure):
     """upe_worker_cfg_t."""
     _fields_ = [("batch", ctypes.c_size_t), ("burst", ctypes.c_uint), ("pool_base", _VP),
-                ("idle_ns", ctypes.c_uint)]
+                ("idle_ns", ctypes.c_uint), ("pool_bytes", ctypes.c_size_t)]
 
 
 class QueueBatch(ctypes.Structure):

@@ -419,9 +419,12 @@ def _v6_pool(rng, k, prefix=bytes.fromhex("20010db8")):
 
 
 def _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, protos4, protos6, ports,
-                 exact_frac=0.0):
+                 exact_frac=0.0, wildcards_last=False):
     """Random 5-tuple rules drawn from the traffic's own pools so they match at spread-out
-    positions; last rule is the catch-all."""
+    positions; last rule is the catch-all.  wildcards_last: a draw that constrains nothing but
+    the IP version (a catch-all for its family) goes after every constraining rule — config C's
+    seed-3 draw has an IPv6 one at priority 1, DROP, which takes every IPv6 packet (so C as
+    SURVEY.md pins it forwards IPv4 only); with it last, IPv6 packets reach the NDP lookup."""
     rules = []
     prios = rng.permutation(n_rules - 1) + 1
     for i in range(n_rules - 1):
@@ -455,12 +458,18 @@ def _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, protos4, protos6,
             kw["dport"] = int(ports[rng.integers(len(ports))])
         if rng.random() < 0.1 and not exact:
             kw["ip_ver"] = 0  # version-agnostic: address bytes apply under both views
+        if wildcards_last and not any(k in kw for k in ("src", "dst", "proto", "sport", "dport")):
+            prios[i] += n_rules
         rules.append(make_rule(int(prios[i]), act, **kw))
     rules.append(make_rule(1 << 30, ACT_DROP))
     return rules_array(rules)
 
 
-def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024) -> Workload:
+def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024,
+             v6_forwarding: bool = False) -> Workload:
+    """BASELINE configs[2] as SURVEY.md §5 pins it (seed 3).  v6_forwarding: the same traffic
+    and rules with the family-wide wildcards moved last (`_mixed_rules` wildcards_last), so
+    that IPv6 packets are forwarded through the NDP lookup (the "C6" variant)."""
     rng = np.random.default_rng(seed)
     n_hosts = 1000
     v4_src = (0x0A000000 + rng.integers(0, 1 << 16, size=n_hosts) * 7).astype(np.uint64)
@@ -473,7 +482,8 @@ def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024) -> Workload:
                            for ip in v4_dst[rng.permutation(n_hosts)[:600]]])
     ndp = ndp_table(1024, [(bytes(ip), _rand_macs(rng, 1)[0].tobytes())
                            for ip in v6_dst[rng.permutation(n_hosts)[:600]]])
-    rules = _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, [17, 6, 1], [17, 6], ports)
+    rules = _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, [17, 6, 1], [17, 6], ports,
+                         wildcards_last=v6_forwarding)
 
     size = rng.choice(np.array([64, 570, 1518]), size=n, p=[7 / 12, 4 / 12, 1 / 12])
     is6 = rng.random(n) < 0.3
