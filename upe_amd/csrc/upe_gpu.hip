@@ -759,9 +759,9 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
             }
         }
     }
-    if (pos == kNone) return kNone;
-    const uint32_t* idx = reinterpret_cast<const uint32_t*>(f6 + (size_t)kFamV6Stride * a.fam6);
-    return idx[(is6 ? a.fam4 : 0u) + pos];
+    // the lane's entry in the lists' index array (fam4 + position for the IPv6 list); the caller
+    // loads the sorted index from it late, so the round trip overlaps the rest of the chunk
+    return pos == kNone ? kNone : (is6 ? a.fam4 : 0u) + pos;
 }
 
 // Key hash of the tuple-space index (host and device agree bit for bit).
@@ -1618,6 +1618,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 ri = need_v6 ? scan_fam<true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6)
                              : scan_fam<false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6);
         }
+        // kFam: ri is the lane's entry in the FamTable index array; the sorted index it holds is
+        // loaded now and first used at the verdict store
+        uint32_t rsi = ri;
+        if (kFam && ri != kNone)
+            rsi = reinterpret_cast<const uint32_t*>(a.fam + 2 * (size_t)a.fam4 +
+                                                    (size_t)kFamV6Stride * a.fam6)[ri];
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
         uint32_t code = 0, rbits = 0;
@@ -1629,7 +1635,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             code = UPE_V_DROP_NOMATCH;
         } else {
             const uint32_t ac = (act >> 16) & 3u;
-            rbits = (ri + 1) << 8;
+            if (!kFam) rbits = (ri + 1) << 8;
             // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: an LDS histogram below for
             // LDS-resident tables; for larger ones upe_rule_hist folds the verdict words after
             // the launch (one scattered device atomic per packet would cost more than the
@@ -1767,6 +1773,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                                 (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
+        if (kFam && ok && !r.consumed && ri != kNone) rbits = (rsi + 1) << 8;
         if (live)   // written through (sc1): no dirty lines left for the boundary
             __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1797,7 +1804,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // the bin's low word counts packets, the high word bytes; neither carries into the other
         // (a workgroup's packets and bytes each fit 32 bits, as the u32 views below assume) ----
         if (lds_stats && !(kAblate & 4) && ok && ri != kNone)
-            atomicAdd(reinterpret_cast<unsigned long long*>(&lds_hist[2 * ri]),
+            atomicAdd(reinterpret_cast<unsigned long long*>(&lds_hist[2 * rsi]),
                       ((unsigned long long)len << 32) | 1ull);
 
         // ---- counters and L1 bookkeeping: ballots, added by one lane into the workgroup's LDS
@@ -3128,11 +3135,25 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     // linear-scan tables past the LDS copy: the per-family lists (FamTable)
     c->fam4 = c->fam6 = 0;
     if (pad > (size_t)kSmallRules) {
+        // each list ends at its first rule that matches every key of its family (nothing after
+        // it can be a first match: config C's IPv6 list is one entry long)
         std::vector<uint32_t> l4, l6;
+        bool end4 = false, end6 = false;
         for (size_t i = 0; i < count; ++i) {
             const uint8_t ver = rules[i].ip_ver;
-            if (ver == 0 || ver == 4) l4.push_back((uint32_t)i);
-            if (ver == 0 || ver == 6) l6.push_back((uint32_t)i);
+            const RuleV4& e = v4[i];
+            const bool all4 = (e.m0 & 0xFFFFFF00u) == 0 && (e.m1 & 0xFFFFu) == 0 && e.sm0 == 0 &&
+                              e.dm0 == 0;
+            bool all6 = all4;
+            for (int j = 0; j < 3; ++j) all6 = all6 && v6[i].sm[j] == 0 && v6[i].dm[j] == 0;
+            if (!end4 && (ver == 0 || ver == 4)) {
+                l4.push_back((uint32_t)i);
+                end4 = all4;
+            }
+            if (!end6 && (ver == 0 || ver == 6)) {
+                l6.push_back((uint32_t)i);
+                end6 = all6;
+            }
         }
         const size_t n4 = (l4.size() + kUnroll - 1) / kUnroll * kUnroll;
         const size_t n6 = (l6.size() + kUnroll - 1) / kUnroll * kUnroll;
