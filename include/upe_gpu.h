@@ -515,7 +515,8 @@ int upe_gpu_batch_info(upe_gpu_ctx_t *ctx, upe_batch_info_t *info);
 typedef struct {
     uint32_t variant;  /* kernel variant: bit 0 emit, 1 tuple space, 2 lean, 3 no look-back,
                           4 ring (stamped), 5 a host path (upe_gpu_process_mapped / _host),
-                          6 a linear-scan table past 64 rules (per-family rule lists) */
+                          6 a linear-scan table past 64 rules (per-family rule lists),
+                          7 the same scanned whole */
     uint32_t grid;     /* workgroups of the launch */
     uint32_t deferred; /* (chunk, family) entries whose look-back was deferred to the last
                           workgroup (0 when the look-back was not live) */

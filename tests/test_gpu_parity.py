@@ -475,3 +475,33 @@ def test_config_c_ipv6_forwarding(gpu_worker_factory, emit):
     is6 = wl.frames[offs + 12] == 0x86
     fwd6 = ((verdict & 0xF) == V_FWD) & is6 & ((verdict & 0x10) != 0)
     assert fwd6.sum() > 1000, "IPv6 packets must be forwarded through the NDP table"
+
+
+@pytest.mark.parametrize("kind", ["C", "C6", "big_linear"])
+def test_linear_scan_flavours(gpu_worker_factory, monkeypatch, kind):
+    """The three ways a linear-scan table past 64 rules is walked, each against the oracle:
+    config C (its IPv6 list is one catch-all: the whole table through the scalar unit), C6
+    (per-family lists, the IPv6 one in LDS, sorted indexes carried in the rule words) and a 16k-rule
+    table with the tuple-space index switched off (per-family lists, sorted indexes from the
+    index array)."""
+    if kind == "big_linear":
+        monkeypatch.setenv("UPE_GPU_TSS", "0")
+        wl = synth.config_d(n=30_000, seed=93, n_rules=1 << 14)
+        want = gpu.VAR_FAM
+    else:
+        wl = synth.config_c(n=40_000, seed=3, v6_forwarding=kind == "C6")   # seed 3: C's rules
+        want = gpu.VAR_GLB if kind == "C" else gpu.VAR_FAM
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w)
+        info = w.launch_info()
+    finally:
+        w.close()
+    assert info["variant"] & (gpu.VAR_FAM | gpu.VAR_GLB) == want
+    r = oracle.run_restated(wl)
+    assert np.array_equal(verdict, r.verdict)
+    assert np.array_equal(frames, r.frames)
+    assert counters.tobytes() == r.counters.tobytes()
+    assert np.array_equal(stats, r.rule_stats)
+    assert l1.tobytes() == r.l1.tobytes()

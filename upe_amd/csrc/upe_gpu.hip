@@ -297,7 +297,8 @@ struct Args {
     const uint4* fam;
     uint32_t fam4, fam6;           // entries per list, multiples of kUnroll
     uint32_t fam6_lds;             // the IPv6 list is staged in LDS (after the neighbour indexes)
-    uint32_t fam_all;              // bit 0 / 1: the IPv4 / IPv6 list is one rule matching every key
+    uint32_t fam_x1idx;            // tables below 8192 rules: each entry's x1 bits 18-30 carry its
+                                   // sorted index (no index-array load after a match)
     uint32_t port_mac_lo, port_mac_hi, port_ip4;
     NeighIndex arp, ndp;
     DevState* st;
@@ -696,11 +697,6 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
     const uint4* f6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t pos = kNone;
     bool dn = done || is6;
-    // a list that is one rule matching every key of its family answers without a test
-    if (a.fam_all & 1u) {
-        if (!dn) { pos = 0; act = f4[0][2]; }
-        dn = true;
-    }
     for (uint32_t b = 0; b < a.fam4; b += kUnroll) {
         if (!__any(!dn)) break;
         const uint32_t base = __builtin_amdgcn_readfirstlane(b);
@@ -716,9 +712,7 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
             }
         }
     }
-    if (V6 && (a.fam_all & 2u)) {
-        if (!(done || !is6)) { pos = 0; act = as_const<u32x8>(f6)[0][2]; }
-    } else if (V6 && a.fam6_lds) {
+    if (V6 && a.fam6_lds) {
         dn = done || !is6;
         for (uint32_t b = 0; b < a.fam6; b += kUnroll) {
             if (!__any(!dn)) break;
@@ -1281,7 +1275,7 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kHost = false, bool kFam = false>
+          bool kHost = false, bool kFam = false, bool kGlb = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1306,7 +1300,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     const bool lds_stats = a.nrules_pad <= (uint32_t)kLdsStatsMax;
     // (kFam: a linear-scan table past kSmallRules, scanned through its family lists; the host
     // picks the instantiation, so the small-table kernels carry no FamTable code)
-    const bool small_stats = !kFam && a.nrules_pad <= (uint32_t)kSmallRules;
+    // kGlb: the same tables scanned whole through the scalar unit (chosen when a family's list is
+    // a single catch-all: there the family split measured slower, config C 39.8 vs 41.9 us)
+    const bool small_stats = !kFam && !kGlb && a.nrules_pad <= (uint32_t)kSmallRules;
 
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
@@ -1620,19 +1616,23 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else {
             // small tables from their LDS copy, larger ones through the scalar unit
             const uint32_t nr = a.nrules_pad;
-            if (!kFam)
-                ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
-                             : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
-            else
+            if (kFam)
                 ri = need_v6 ? scan_fam<true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6)
                              : scan_fam<false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6);
+            else if (kGlb)
+                ri = need_v6 ? scan_rules<true, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
+                             : scan_rules<false, false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
+            else
+                ri = need_v6 ? scan_rules<true, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr)
+                             : scan_rules<false, true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_rv4, s_rv6, 0u, nr);
         }
         // kFam: ri is the lane's entry in the FamTable index array; the sorted index it holds is
         // loaded now and first used at the verdict store
         uint32_t rsi = ri;
         if (kFam && ri != kNone)
-            rsi = reinterpret_cast<const uint32_t*>(a.fam + 2 * (size_t)a.fam4 +
-                                                    (size_t)kFamV6Stride * a.fam6)[ri];
+            rsi = a.fam_x1idx ? (act >> 18) & 0x1FFFu
+                              : reinterpret_cast<const uint32_t*>(a.fam + 2 * (size_t)a.fam4 +
+                                                                  (size_t)kFamV6Stride * a.fam6)[ri];
 
         // ---- verdict, counters, rule_stats (src/worker.c:117-153) ----
         uint32_t code = 0, rbits = 0;
@@ -2321,6 +2321,7 @@ struct upe_gpu_ctx {
     size_t fam_alloc = 0;                      // bytes
     uint32_t fam4 = 0, fam6 = 0;
     uint32_t fam_all = 0;
+    uint32_t fam_x1idx = 0;
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
@@ -2565,25 +2566,27 @@ int arm_state(upe_gpu_ctx* c) {
 
 hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
-constexpr int kVarCount = 128;
+constexpr int kVarCount = 256;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
-// upe_gpu_process_host; not ring), bit 6 a linear-scan table past kSmallRules (FamTable; not
-// tuple space).
+// upe_gpu_process_host; not ring), bit 6 a linear-scan table past kSmallRules scanned through
+// its family lists (FamTable), bit 7 the same scanned whole (neither with tuple space).
 enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
-       VAR_FAM = 64 };
+       VAR_FAM = 64, VAR_GLB = 128 };
+// scan: 0 small table (LDS copy), 1 family lists, 2 whole table through the scalar unit
 int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
-                 bool fam = false) {
-    return (fam && !tss ? VAR_FAM : 0) | (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) |
-           (lean && nolb ? VAR_NOLB : 0) | (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) |
-           (emit ? VAR_EMIT : 0);
+                 int scan = 0) {
+    return (!tss && scan == 1 ? VAR_FAM : 0) | (!tss && scan == 2 ? VAR_GLB : 0) |
+           (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) |
+           (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
 }
 // The instantiated variants (every combination classify_var can return for a launch).
 constexpr bool var_built(int v) {
     const bool emit = v & VAR_EMIT, lean = v & VAR_LEAN, nolb = v & VAR_NOLB, ring = v & VAR_RING,
                host = v & VAR_HOST;
     if (nolb && !lean) return false;
-    if ((v & VAR_FAM) && (v & VAR_TSS)) return false;
+    if ((v & (VAR_FAM | VAR_GLB)) && (v & VAR_TSS)) return false;
+    if ((v & VAR_FAM) && (v & VAR_GLB)) return false;
     if (ring) return !host && emit && lean && !(v & VAR_TSS);
     return true;
 }
@@ -2593,7 +2596,7 @@ const void* classify_fn_of() {
         return reinterpret_cast<const void*>(
             &upe_classify<(V & VAR_TSS) != 0, (V & VAR_EMIT) != 0, (V & VAR_LEAN) != 0,
                           (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0,
-                          (V & VAR_FAM) != 0>);
+                          (V & VAR_FAM) != 0, (V & VAR_GLB) != 0>);
     else
         return nullptr;
 }
@@ -3145,6 +3148,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     // linear-scan tables past the LDS copy: the per-family lists (FamTable)
     c->fam4 = c->fam6 = 0;
     c->fam_all = 0;
+    c->fam_x1idx = 0;
     if (pad > (size_t)kSmallRules) {
         // each list ends at its first rule that matches every key of its family (nothing after
         // it can be a first match: config C's IPv6 list is one entry long)
@@ -3176,15 +3180,21 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         never.x0 = 0xFF;   // ip_ver byte 0xFF against a key version of 4 or 6
         never.m0 = 0xFF;
         uint32_t* idx = reinterpret_cast<uint32_t*>(img.data() + 2 * n4 + kFamV6Stride * n6);
+        // tables below 8192 rules: the sorted index rides in x1 bits 18-30 (m1 keeps them clear,
+        // so the match is unchanged) and comes back with the matched rule's words
+        const bool x1idx = count < 8192;
         for (size_t j = 0; j < n4; ++j) {
-            const RuleV4& e = j < l4.size() ? v4[l4[j]] : never;
+            RuleV4 e = j < l4.size() ? v4[l4[j]] : never;
+            if (x1idx && j < l4.size()) e.x1 |= l4[j] << 18;
             memcpy(&img[2 * j], &e, sizeof e);
             idx[j] = j < l4.size() ? l4[j] : 0u;
         }
         for (size_t j = 0; j < n6; ++j) {
             uint4* o = &img[2 * n4 + kFamV6Stride * j];
             if (j < l6.size()) {
-                memcpy(o, &v4[l6[j]], sizeof(RuleV4));
+                RuleV4 e = v4[l6[j]];
+                if (x1idx) e.x1 |= l6[j] << 18;
+                memcpy(o, &e, sizeof(RuleV4));
                 memcpy(o + 2, &v6[l6[j]], 3 * sizeof(uint4));   // s, sm, d, dm (12 words)
             } else {
                 memcpy(o, &never, sizeof never);
@@ -3203,6 +3213,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         c->fam4 = (uint32_t)n4;
         c->fam6 = (uint32_t)n6;
         c->fam_all = (l4.size() == 1 && end4 ? 1u : 0u) | (l6.size() == 1 && end6 ? 2u : 0u);
+        c->fam_x1idx = x1idx ? 1u : 0u;
     }
     c->nrules = (uint32_t)count;
     c->nrules_pad = (uint32_t)pad;
@@ -3491,7 +3502,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.fam = c->fam;
     a.fam4 = c->fam4;
     a.fam6 = c->fam6;
-    a.fam_all = c->fam_all;
+    a.fam_x1idx = c->fam_x1idx;
     a.rinfo = c->rinfo;
     a.nrules_pad = c->nrules_pad;
     a.arp = arp_index(c);
@@ -3557,7 +3568,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         lds += c->nfs * sizeof(uint4);
     }
     a.fam6_lds = 0u;
-    if (kFamLds && !c->tss && c->fam6 && lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
+    if (kFamLds && !c->tss && !c->fam_all && c->fam6 &&
+        lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
         a.fam6_lds = 1u;
         lds += kFamV6Stride * c->fam6 * sizeof(uint4);
     }
@@ -3581,15 +3593,17 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     // (at most kRingMax batches: one LDS counter each)
     bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
-    const bool fam = !c->tss && c->nrules_pad > (uint32_t)kSmallRules;
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, fam);
+    // large linear tables: family lists, unless a family's list is a single catch-all (then the
+    // split gains that family nothing and measured slower for the other)
+    const int scan = c->tss || c->nrules_pad <= (uint32_t)kSmallRules ? 0 : c->fam_all ? 2 : 1;
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, scan);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host, fam), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host, scan), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -3606,7 +3620,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         const size_t tpb = (ring->per / 64) / tw;
         if (stamp && (tpb < grid || tpb % grid != 0)) stamp = false;
         if (!stamp) {
-            var = classify_var(c->tss, emit, lean, c->no_lb, false, false, fam);
+            var = classify_var(c->tss, emit, lean, c->no_lb, false, false, scan);
             if (resident_grid(c, var, lds, s) == 0) return -1;
         } else {
             const size_t nb = n / ring->per;

@@ -28,6 +28,7 @@ VAR_NOLB = 8    # the kernel without look-back
 VAR_RING = 16   # a ring launch whose batches are stamped
 VAR_HOST = 32   # a host path's launch (mapped host memory, host round trip)
 VAR_FAM = 64    # a linear-scan table past 64 rules, scanned through per-family rule lists
+VAR_GLB = 128   # the same scanned whole (a family's list is a single catch-all)
 
 
 # upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
