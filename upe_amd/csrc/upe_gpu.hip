@@ -723,7 +723,9 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
                 const uint4 e0 = e[0], e1 = e[1];
                 uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
                              ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
-                if (__builtin_amdgcn_readfirstlane(e0.w) & kRuleV6Words) {
+                // (the IPv6 words only when some lane still looking passes the rest of the rule:
+                // C6 136.6 -> 126.9 us; in the whole-table scan the same test cost C 0.5 us)
+                if ((__builtin_amdgcn_readfirstlane(e0.w) & kRuleV6Words) && __any(!dn && x == 0)) {
                     const uint4 e2 = e[2], e3 = e[3], e4 = e[4];
                     // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3
                     x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
@@ -748,7 +750,7 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
                 const u32x8 r = *as_const<u32x8>(e);
                 uint32_t x = ((k0 ^ r[0]) & r[1]) | ((k1 ^ r[2]) & r[3]) |
                              ((s[0] ^ r[4]) & r[5]) | ((d[0] ^ r[6]) & r[7]);
-                if (__builtin_amdgcn_readfirstlane(r[3]) & kRuleV6Words) {
+                if ((__builtin_amdgcn_readfirstlane(r[3]) & kRuleV6Words) && __any(!dn && x == 0)) {
                     const u32x16 q = *as_const<u32x16>(e + 2);
                     x |= ((s[1] ^ q[0]) & q[3]) | ((s[2] ^ q[1]) & q[4]) | ((s[3] ^ q[2]) & q[5]) |
                          ((d[1] ^ q[6]) & q[9]) | ((d[2] ^ q[7]) & q[10]) | ((d[3] ^ q[8]) & q[11]);
