@@ -150,3 +150,56 @@ def test_reload_in_a_stream_of_batches(gpu_worker_factory, host):
                  {"verdict": ref.verdict, "frames": ref.frames, "counters": ref.counters,
                   "rule_stats": ref.rule_stats, "l1": ref.l1}, f"stream reload host={host}",
                  batch_relative=True)
+
+
+def test_reload_returns_to_lookback(gpu_worker_factory, monkeypatch):
+    """A family that no reachable rule forwards never consults its L1 entry, so a disagreeing
+    entry of that family does not keep the look-back kernel (config C's table: IPv6 all dropped at
+    rule 0).  A reload that lets that family forward must bring the look-back back: here the
+    starting NDP entry holds a wrong MAC for the destination of the first IPv6 packet the new
+    table forwards, which must take the entry's MAC as in the reference worker."""
+    from upe_amd.layout import V_FWD, desc_offsets
+
+    monkeypatch.setenv("UPE_GPU_LB_SYNC", "1")
+    n, at = 60_000, 30_000
+    wa = synth.config_c(n=n, seed=3)
+    w6 = synth.config_c(n=n, seed=3, v6_forwarding=True)
+    part2 = w6.copy()
+    part2.desc = w6.desc[at:]
+    r2 = oracle.run_restated(part2)
+    offs = desc_offsets(part2.desc)
+    is6 = part2.frames[offs + 12] == 0x86
+    k = int(np.nonzero(is6 & ((r2.verdict & 0xF) == V_FWD))[0][0])
+    l1 = synth.l1_zero()
+    l1["last_ndp_ip"] = part2.frames[offs[k] + 38: offs[k] + 54]
+    l1["last_ndp_mac"] = [2, 0, 0, 0, 0, 1]
+    wa.l1 = l1
+    ref, _ = oracle.run_reference_reload(wa, w6.rules, w6.capacity, at)
+    w = gpu_worker_factory(wa.capacity)
+    variants = []
+    try:
+        w.configure(wa)
+        frames = wa.frames
+        verdicts = []
+        for s, e in ((0, 10_000), (10_000, 20_000), (20_000, at), (at, n)):
+            if s == at:
+                w.reload_rules(ref.rules_sorted, w6.capacity)
+            b = gpu.DeviceBatch(w, frames, wa.desc[s:e])
+            b.run()
+            frames, v = b.fetch()
+            b.free()
+            verdicts.append(v)
+            variants.append(w.launch_info()["variant"])
+        counters, stats = w.get_stats()
+        l1_out = w.get_l1()
+    finally:
+        w.close()
+    assert variants[2] & gpu.VAR_NOLB, variants             # IPv6 cannot forward under table A
+    assert not variants[3] & gpu.VAR_NOLB, variants         # ... and can under table B
+    verdict = np.concatenate(verdicts)
+    _assert_same((frames, verdict, counters, stats, l1_out),
+                 {"verdict": ref.verdict, "frames": ref.frames, "counters": ref.counters,
+                  "rule_stats": ref.rule_stats, "l1": ref.l1}, "reload to IPv6 forwarding",
+                 batch_relative=True)
+    hit = ref.verdict[at + k]
+    assert (hit & 0xF) == V_FWD and hit & 0x10, "the aimed packet is forwarded with a MAC"

@@ -2323,6 +2323,9 @@ struct upe_gpu_ctx {
     size_t fam_alloc = 0;                      // bytes
     uint32_t fam4 = 0, fam6 = 0;
     uint32_t fam_all = 0;
+    // whether a packet of each family can be forwarded at all under the current table: some
+    // rule it can reach first (up to its family's first catch-all) forwards
+    bool fwd4 = true, fwd6 = true;
     uint32_t fam_x1idx = 0;
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
@@ -3148,6 +3151,27 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     HIP_TRY(hipMemcpy(c->rv6, v6.data(), pad * sizeof(RuleV6), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->rinfo, info.data(), pad * sizeof(int2), hipMemcpyHostToDevice));
     // linear-scan tables past the LDS copy: the per-family lists (FamTable)
+    // a family none of whose reachable rules forwards never consults or updates its L1 entry
+    // (src/worker.c:155-244 run only for forwarded packets): its entry's agreement is moot
+    {
+        bool e4 = false, e6 = false;
+        c->fwd4 = c->fwd6 = false;
+        for (size_t i = 0; i < count && !(e4 && e6); ++i) {
+            const uint8_t ver = rules[i].ip_ver;
+            const RuleV4& e = v4[i];
+            const bool all4 = (e.m0 & 0xFFFFFF00u) == 0 && (e.m1 & 0xFFFFu) == 0 && e.sm0 == 0 &&
+                              e.dm0 == 0;
+            bool all6 = all4;
+            for (int j = 0; j < 3; ++j) all6 = all6 && v6[i].sm[j] == 0 && v6[i].dm[j] == 0;
+            const bool fwd = rules[i].action.type == UPE_ACT_FWD;
+            if (!e4 && (ver == 0 || ver == 4)) { c->fwd4 = c->fwd4 || fwd; e4 = all4; }
+            if (!e6 && (ver == 0 || ver == 6)) { c->fwd6 = c->fwd6 || fwd; e6 = all6; }
+        }
+        // the kernel without look-back may have been chosen because a family could not forward
+        // under the old table: back to the full kernel until a launch under this one reports
+        c->no_lb = false;
+        c->lb_reset_k = c->k;
+    }
     c->fam4 = c->fam6 = 0;
     c->fam_all = 0;
     c->fam_x1idx = 0;
@@ -3586,8 +3610,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             HIP_TRY(hipStreamSynchronize(c->last_stream));   // the previous launch's report
         const unsigned long long v = __atomic_load_n(c->agree_h, __ATOMIC_ACQUIRE);
         const unsigned long long tag = v >> 2;
-        if (tag != 0 && tag - 1 >= c->lb_reset_k && ((v & 1) || c->arp_bits == 0) &&
-            ((v & 2) || c->ndp_bits == 0))
+        if (tag != 0 && tag - 1 >= c->lb_reset_k && ((v & 1) || c->arp_bits == 0 || !c->fwd4) &&
+            ((v & 2) || c->ndp_bits == 0 || !c->fwd6))
             c->no_lb = true;
     }
     a.agree_out = c->no_lb ? nullptr : c->agree_d;
