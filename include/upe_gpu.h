@@ -214,11 +214,32 @@ int upe_gpu_load_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count
 int upe_gpu_reload_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count,
                          size_t rule_capacity, upe_rule_stat_t *old_stats, size_t old_capacity);
 
-/* How the loaded table is classified: 0 = linear first-match scan (small tables, or many mask
- * signatures), 1 = tuple-space index (large tables whose rules fall into few mask signatures:
- * one hash probe per signature, visited in order of each signature's first rule, so the result
- * is still the first match in (priority, rule_id) order).  -1 on error. */
+/* How the loaded table is classified: 0 = linear first-match scan (tables of up to 64 rules, or
+ * a table whose tree outgrew its node budget), 1 = tuple-space index (large tables whose rules
+ * fall into few mask signatures: one hash probe per signature, visited in order of each
+ * signature's first rule), 2 = decision tree over the per-family rule lists (every other table
+ * past 64 rules: a walk to a leaf, then the few rules listed there in order).  Each gives the
+ * first match in (priority, rule_id) order (reference src/rule_table.c:163-176).  -1 on error. */
 int upe_gpu_rule_index_kind(upe_gpu_ctx_t *ctx);
+
+/* The decision tree of the loaded table (all zero when it has none). */
+typedef struct {
+    uint64_t nodes;        /* nodes of both families' trees */
+    uint64_t leaf_entries; /* rule positions listed in the leaves */
+    uint32_t depth4;       /* deepest leaf of the IPv4 tree */
+    uint32_t depth6;       /* deepest leaf of the IPv6 tree */
+    uint32_t max_leaf;     /* longest leaf list */
+    uint32_t trees;        /* trees of the IPv4 forest | trees of the IPv6 forest << 16 */
+} upe_rule_index_info_t;
+int upe_gpu_rule_index_info(upe_gpu_ctx_t *ctx, upe_rule_index_info_t *info);
+
+/* rule_table_match (reference src/rule_table.c:163-176) over n keys on the host, through the
+ * decision tree the GPU path builds for rules[0..count) (sorted as for upe_gpu_load_rules; the
+ * walk is the device's, bit for bit), or the per-family linear first match when the table gets
+ * no tree.  out[i] = the sorted index of keys[i]'s first matching rule, or -1 (no match, or an
+ * ip_ver other than 4 / 6).  info (optional): the tree's shape.  No GPU needed.  0 / -1. */
+int upe_rules_match_host(const upe_rule_t *rules, size_t count, const upe_flow_key_t *keys,
+                         size_t n, int64_t *out, upe_rule_index_info_t *info);
 
 /* Upload a snapshot of the neighbour tables' slot arrays (arpt->entries / ndpt->entries with
  * their power-of-two capacities).  Lookups probe exactly as arp_get_mac/ndp_get_mac do.

@@ -70,7 +70,7 @@ def _assert_same(got, ref, what="", batch_relative=False):
 
 @pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
-                                  "config_d_small"])
+                                  "config_cf_small", "config_d_small"])
 def test_golden_no_control(gpu_worker_factory, case, emit):
     wl, ref = golden_io.load(case)
     _assert_same(_run(gpu_worker_factory, wl, emit=emit), ref, f"{case} emit={emit}")
@@ -271,6 +271,10 @@ def _sha(*arrays):
     ("C_1M", lambda: synth.config_c(), True),
     ("D_256k_64k_rules", lambda: synth.config_d(n=1 << 18), False),
     ("D_256k_64k_rules", lambda: synth.config_d(n=1 << 18), True),
+    ("CF_1M", lambda: synth.config_c_flows(), False),
+    ("CF_1M", lambda: synth.config_c_flows(), True),
+    ("C6_1M", lambda: synth.config_c(v6_forwarding=True), False),
+    ("C6_1M", lambda: synth.config_c(v6_forwarding=True), True),
 ])
 def test_full_size_digest(gpu_worker_factory, key, make, emit):
     """BASELINE.json full sizes against SHA-256 digests of the reference worker's outputs."""
@@ -362,22 +366,28 @@ def test_lookback_far_first_hit(gpu_worker_factory, n, first_hit, emit):
                        "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "1-unstaged"])
+@pytest.mark.parametrize("mode", ["scan", "tree", "tree-memory", "tss", "tss-unstaged"])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
-                                  "config_d_small", "edge_inconsistent"])
+                                  "config_cf_small", "config_d_small", "edge_inconsistent"])
 def test_rule_index_kinds_agree(gpu_worker_factory, monkeypatch, case, mode):
-    """Both classifiers — the linear first-match scan and the tuple-space index — forced on
-    every fixture (version-0 rules, mixed v4/v6 masks, wildcard fields, catch-alls) give the
-    reference's first match; the tuple-space probes both with small groups' fingerprints in LDS
-    and with none staged (every group probed slot by slot)."""
-    monkeypatch.setenv("UPE_GPU_TSS", mode[0])
+    """Every classifier — the linear first-match scan, the decision tree over the family lists
+    (its image staged in LDS, or read from memory) and the tuple-space index (small groups'
+    fingerprints in LDS, or none staged) — forced on every fixture (version-0 rules, mixed v4/v6
+    masks, wildcard fields, catch-alls) gives the reference's first match."""
+    monkeypatch.setenv("UPE_GPU_TSS", "1" if mode.startswith("tss") else "0")
+    monkeypatch.setenv("UPE_GPU_TREE", "0" if mode == "scan" else "1")
+    monkeypatch.setenv("UPE_GPU_TREE_LDS", "0" if mode == "tree-memory" else "1")
     monkeypatch.setenv("UPE_GPU_FP_STAGE", "0" if mode.endswith("unstaged") else "1")
     wl, ref = golden_io.load(case)
     w = gpu_worker_factory(wl.capacity)
     try:
         w.configure(wl)
-        assert w.rule_index_kind() == int(mode[0])
+        big = len(wl.rules) > 64
+        assert w.rule_index_kind() == (1 if mode.startswith("tss") else
+                                       2 if mode.startswith("tree") and big else 0)
         frames, verdict, counters, stats, l1 = gpu.run_workload(wl, worker=w)
+        if mode.startswith("tree") and big:
+            assert w.launch_info()["variant"] & gpu.VAR_SCAN == gpu.VAR_TREE
     finally:
         w.close()
     if case.startswith("edge"):
@@ -385,7 +395,7 @@ def test_rule_index_kinds_agree(gpu_worker_factory, monkeypatch, case, mode):
         r = oracle.run_restated(wl, apply_control=False)
         ref = {"verdict": r.verdict, "frames": r.frames, "counters": r.counters,
                "rule_stats": r.rule_stats, "l1": r.l1}
-    _assert_same((frames, verdict, counters, stats, l1), ref, f"{case} tss={mode}")
+    _assert_same((frames, verdict, counters, stats, l1), ref, f"{case} {mode}")
 
 
 def test_config_d_uses_tuple_space(gpu_worker_factory):
@@ -477,20 +487,28 @@ def test_config_c_ipv6_forwarding(gpu_worker_factory, emit):
     assert fwd6.sum() > 1000, "IPv6 packets must be forwarded through the NDP table"
 
 
-@pytest.mark.parametrize("kind", ["C", "C6", "big_linear"])
-def test_linear_scan_flavours(gpu_worker_factory, monkeypatch, kind):
-    """The three ways a linear-scan table past 64 rules is walked, each against the oracle:
-    config C (its IPv6 list is one catch-all: the whole table through the scalar unit), C6
-    (per-family lists, the IPv6 one in LDS, sorted indexes carried in the rule words) and a 16k-rule
-    table with the tuple-space index switched off (per-family lists, sorted indexes from the
-    index array)."""
+@pytest.mark.parametrize("tree", [False, True])
+@pytest.mark.parametrize("kind", ["C", "C6", "CF", "big_linear"])
+def test_linear_scan_flavours(gpu_worker_factory, monkeypatch, kind, tree):
+    """The ways a linear table past 64 rules is matched, each against the oracle.  Without the
+    tree (UPE_GPU_TREE=0): seed-3 config C (its IPv6 list is one catch-all: the whole table
+    through the scalar unit), C6 and the flow-derived C (per-family lists, the IPv6 one in LDS,
+    sorted indexes carried in the rule words) and a 16k-rule table with the tuple-space index
+    switched off (per-family lists, sorted indexes from the index array).  With it (the default):
+    every one through the decision tree."""
+    monkeypatch.setenv("UPE_GPU_TREE", "1" if tree else "0")
     if kind == "big_linear":
         monkeypatch.setenv("UPE_GPU_TSS", "0")
         wl = synth.config_d(n=30_000, seed=93, n_rules=1 << 14)
         want = gpu.VAR_FAM
+    elif kind == "CF":
+        wl = synth.config_c_flows(n=40_000, seed=5)
+        want = gpu.VAR_FAM
     else:
         wl = synth.config_c(n=40_000, seed=3, v6_forwarding=kind == "C6")   # seed 3: C's rules
         want = gpu.VAR_GLB if kind == "C" else gpu.VAR_FAM
+    if tree:
+        want = gpu.VAR_TREE
     w = gpu_worker_factory(wl.capacity)
     try:
         w.configure(wl)
@@ -498,8 +516,55 @@ def test_linear_scan_flavours(gpu_worker_factory, monkeypatch, kind):
         info = w.launch_info()
     finally:
         w.close()
-    assert info["variant"] & (gpu.VAR_FAM | gpu.VAR_GLB) == want
+    assert info["variant"] & gpu.VAR_SCAN == want
     r = oracle.run_restated(wl)
+    assert np.array_equal(verdict, r.verdict)
+    assert np.array_equal(frames, r.frames)
+    assert counters.tobytes() == r.counters.tobytes()
+    assert np.array_equal(stats, r.rule_stats)
+    assert l1.tobytes() == r.l1.tobytes()
+
+
+def _mixed_table(n_rules: int, seed: int):
+    """A config-C-style table of n_rules random rules (synth._mixed_rules: prefixes /8-/32 and
+    /32-/128 drawn from the traffic's host pools, ports exact or 0, 10 % version-agnostic):
+    thousands of mask signatures, so neither the tuple-space index nor an LDS copy applies."""
+    rng = np.random.default_rng(seed)
+    n_hosts = 1000
+    v4_src = (0x0A000000 + rng.integers(0, 1 << 16, size=n_hosts) * 7).astype(np.uint64)
+    v4_dst = (0xAC100000 + rng.integers(0, 1 << 12, size=n_hosts)).astype(np.uint64)
+    v6_src = synth._v6_pool(rng, n_hosts)
+    v6_dst = synth._v6_pool(rng, n_hosts, prefix=bytes.fromhex("2001db80"))
+    ports = np.concatenate([np.array([53, 80, 443, 22, 123, 8080]),
+                            rng.integers(1024, 65536, size=200)])
+    return synth._mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, [17, 6, 1], [17, 6],
+                              ports)
+
+
+@pytest.mark.parametrize("emit", [False, True])
+@pytest.mark.parametrize("table", ["mixed_64k", "flows_16k"])
+def test_large_linear_tables(gpu_worker_factory, table, emit):
+    """Tables with many mask signatures past the LDS (the tuple-space index declines them), so
+    the decision tree is read from memory: a 64k-rule config-C-style random table over config C's
+    traffic (early first matches), and a 16k-rule flow-derived table whose first matches spread
+    over the whole table (deep scans for the reference) — against the oracle on 20k packets."""
+    if table == "mixed_64k":
+        wl = synth.config_c(n=20_000, seed=61)
+        wl.rules = _mixed_table(1 << 16, 61)
+        wl.capacity = 1 << 16
+    else:
+        wl = synth.config_c_flows(n=20_000, seed=62, n_rules=1 << 14, max_cover=2.0 ** -18)
+    key = ("large", table)
+    if key not in _D_CACHE:
+        _D_CACHE[key] = oracle.run_restated(wl)
+    r = _D_CACHE[key]
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        assert w.rule_index_kind() == 2
+        frames, verdict, counters, stats, l1 = _run(gpu_worker_factory, wl, emit=emit)
+    finally:
+        w.close()
     assert np.array_equal(verdict, r.verdict)
     assert np.array_equal(frames, r.frames)
     assert counters.tobytes() == r.counters.tobytes()

@@ -63,6 +63,7 @@
 
 #include <algorithm>
 #include <array>
+#include <deque>
 #include <map>
 #include <atomic>
 #include <new>
@@ -284,6 +285,32 @@ constexpr uint32_t kFpStageGroup = 4096;   // largest group (slots) staged
 // us); a miss takes two slot reads.
 constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 
+// Decision-tree index of a linear-scan table past kSmallRules (round 5; built by
+// upe_gpu_load_rules when the tuple-space index does not apply).  The family lists (FamTable)
+// stay the rules; each list gets a binary tree over the key's words, HyperSplit-style: an inner
+// node compares one key word with a threshold, a leaf lists the positions of the rules whose
+// conservative range meets the leaf's box (lo = x & m, hi = x | ~m per word), in list order, cut
+// after the first one that matches every key of the box (flagged: it needs no test).  A key's
+// first match in (priority, rule_id) order is therefore the first of its leaf's rules that
+// matches it (reference src/rule_table.c:163-176): a rule that can match the key meets the box,
+// so it is listed, or the flagged rule precedes it and matches the key too.  A lane walks its
+// family's tree (one node load per level) and tests a handful of rules, however deep its first
+// match lies in the table — the wave-uniform scan lasted as long as the wave's deepest lane.
+// Key words: 0-3 source address, 4-7 destination address (IPv6: the wire bytes as big-endian
+// words, so that a prefix is a range; IPv4: word 0 host order as parse_flow_key stores it, the
+// other words 0), 8 source port, 9 destination port, 10 protocol.
+//   node (uint2): inner {dim | child << 5, threshold}: key word < threshold -> child, else child+1
+//                 leaf  {16 | count << 5, first entry}
+//   leaf entry (u32): list position | 0x80000000 when the rule matches every key of the leaf
+// Each family's rules are split into groups by the key word on which each is narrowest, one
+// tree per group (a rule narrow only in a port is then not copied into every leaf of a tree cut on
+// addresses); a key's first match is the smallest of its first matches over its family's trees.
+// Image: a directory (node 0 = {IPv4 trees, IPv6 trees}, then a copy of each tree's root, IPv4
+// first), the nodes, then the leaf entries; staged in LDS when it fits beside the launch's other
+// LDS data.
+constexpr int kTreeDims = 11;
+constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
+
 struct Args {
     uint8_t* frames;
     const uint64_t* desc;
@@ -299,6 +326,10 @@ struct Args {
     uint32_t fam6_lds;             // the IPv6 list is staged in LDS (after the neighbour indexes)
     uint32_t fam_x1idx;            // tables below 8192 rules: each entry's x1 bits 18-30 carry its
                                    // sorted index (no index-array load after a match)
+    // decision-tree index over the family lists (kTreeDims comment)
+    const uint2* tree;             // nodes, then the leaf entries (u32) from word tree_loff
+    uint32_t tree_loff;            // leaf entries' offset in u32 words
+    uint32_t tree_lds;             // the image is staged in LDS (uint4 count), 0 = read from memory
     uint32_t port_mac_lo, port_mac_hi, port_ip4;
     NeighIndex arp, ndp;
     DevState* st;
@@ -413,7 +444,7 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8
 __device__ __forceinline__ uint32_t at2(uint32_t hi, uint32_t lo) {   // dword at byte 4q+2
     return __builtin_amdgcn_alignbit(hi, lo, 16);
 }
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 // Mask of the bytes of dword j that lie below len (a zero-filled pktbuf reads 0 past len).
 __device__ __forceinline__ uint32_t len_mask(uint32_t len, int j) {
     const uint32_t lo = 4u * (uint32_t)j;
@@ -766,6 +797,87 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
     // the lane's entry in the lists' index array (fam4 + position for the IPv6 list); the caller
     // loads the sorted index from it late, so the round trip overlaps the rest of the chunk
     return pos == kNone ? kNone : (is6 ? a.fam4 : 0u) + pos;
+}
+
+// First match through the decision-tree index (kTreeDims comment): for each tree of its
+// family's forest a lane walks to a leaf, then tests the leaf's rules in list order against their
+// FamTable entries (the flagged one without a test), stopping at its first match or at a
+// position no better than the best so far.  Walks are per lane (divergent loads: LDS when the
+// image is staged, else memory); the wave iterates as long as its deepest walk and its longest
+// leaf, tree by tree.  Returns the lane's FamTable index-array entry, as scan_fam.
+template <bool kLdsTree>
+__device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool is6, uint32_t k0,
+                                               uint32_t k1, const uint32_t s[4], const uint32_t d[4],
+                                               uint32_t& act, const uint2* lnodes, const uint4* l6) {
+    const uint2* N = kLdsTree ? lnodes : a.tree;
+    const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
+    const uint2 dir = N[0];
+    const uint32_t ntw = __builtin_amdgcn_readfirstlane(dir.x > dir.y ? dir.x : dir.y);
+    const uint32_t nt = active ? (is6 ? dir.y : dir.x) : 0u, first = 1u + (is6 ? dir.x : 0u);
+    // key word `dim`: address words raw (IPv6 byte-swapped below), ports and protocol from k0/k1
+    const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
+    const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
+    uint32_t best = kNone, bact = 0;
+    for (uint32_t t = 0; t < ntw; ++t) {
+        uint2 nd = make_uint2(16u, 0u);   // lanes without a tree t: an empty leaf
+        if (t < nt) nd = N[first + t];
+        while (__any(!(nd.x & 16u))) {
+            if (!(nd.x & 16u)) {
+                // (bit selects, so that the key words stay in registers: a select between
+                // elements of s / d becomes an indexed load of a scratch copy otherwise)
+                const uint32_t dim = nd.x & 15u;
+                const uint32_t m1 = 0u - (dim & 1u), m2 = 0u - ((dim >> 1) & 1u);
+                const uint32_t m4 = 0u - ((dim >> 2) & 1u), m8 = 0u - ((dim >> 3) & 1u);
+                const uint32_t sa = vsel(m2, vsel(m1, s[3], s[2]), vsel(m1, s[1], s[0]));
+                const uint32_t da = vsel(m2, vsel(m1, d[3], d[2]), vsel(m1, d[1], d[0]));
+                uint32_t v = vsel(m4, da, sa);
+                if (is6) v = bswap32(v);
+                v = vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), v);
+                nd = N[(nd.x >> 5) + (v >= nd.y ? 1u : 0u)];
+            }
+        }
+        const uint32_t cnt = nd.x >> 5;
+        bool look = cnt != 0u;
+        for (uint32_t j = 0; __any(look); ++j) {
+            if (look) {
+                const uint32_t e = E[nd.y + j];
+                const uint32_t p = e & 0x7FFFFFFFu;
+                if (p >= best) {
+                    look = false;   // the lists ascend: nothing later in this leaf can win
+                } else {
+                    uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
+                    const bool cov = (e >> 31) != 0u;
+                    if (is6 && a.fam6_lds) {
+                        const uint4* f = l6 + kFamV6Stride * p;
+                        e0 = f[0];
+                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                    } else if (is6) {
+                        const uint4* f = g6 + (size_t)kFamV6Stride * p;
+                        e0 = f[0];
+                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                    } else {
+                        const uint4* f = a.fam + 2 * (size_t)p;
+                        e0 = f[0];
+                        if (!cov) e1 = f[1];
+                    }
+                    uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                                 ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
+                    // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3 (zero words for IPv4 entries)
+                    x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+                         ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+                    if (cov || x == 0u) {
+                        best = p;
+                        bact = e0.z;
+                        look = false;
+                    } else if (j + 1u >= cnt) {
+                        look = false;
+                    }
+                }
+            }
+        }
+    }
+    act = bact;
+    return best == kNone ? kNone : (is6 ? a.fam4 : 0u) + best;
 }
 
 // Key hash of the tuple-space index (host and device agree bit for bit).
@@ -1277,8 +1389,13 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
-          bool kHost = false, bool kFam = false, bool kGlb = false>
+          bool kHost = false, int kScan = 0>
 __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
+    // rule match of a linear-scan table (kScan; the host picks the instantiation, so no kernel
+    // carries another flavour's code): 0 small table from its LDS copy, 1 family lists, 2 whole
+    // table through the scalar unit, 3 decision tree over the family lists
+    constexpr bool kFam = kScan == 1, kGlb = kScan == 2, kTree = kScan == 3;
+    constexpr bool kFamIdx = kFam || kTree;   // the match is a FamTable index-array entry
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
     __shared__ uint32_t s_tot[C_N + 3];   // the workgroup's counters; first f4 / f6 / ctrl (min)
@@ -1300,11 +1417,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const bool lds_stats = a.nrules_pad <= (uint32_t)kLdsStatsMax;
-    // (kFam: a linear-scan table past kSmallRules, scanned through its family lists; the host
-    // picks the instantiation, so the small-table kernels carry no FamTable code)
-    // kGlb: the same tables scanned whole through the scalar unit (chosen when a family's list is
-    // a single catch-all: there the family split measured slower, config C 39.8 vs 41.9 us)
-    const bool small_stats = !kFam && !kGlb && a.nrules_pad <= (uint32_t)kSmallRules;
+    // (kGlb is chosen when a family's list is a single catch-all: there the family split
+    // measured slower, config C 39.8 vs 41.9 us)
+    const bool small_stats = kScan == 0 && a.nrules_pad <= (uint32_t)kSmallRules;
 
     if (lds_stats)
         for (uint32_t r = tid; r < 2 * a.nrules_pad; r += kBlock) lds_hist[r] = 0;
@@ -1401,12 +1516,18 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     uint4* s_fp4 = s_ndp + 2 * a.ndp_lds;
     if (kTssMode)
         for (uint32_t k = tid; k < a.fp_lds; k += kBlock) s_fp4[k] = a.tfs[k];
+    // the decision tree's image, when the host found room for it
+    uint4* s_tree = s_fp4;
+    if (kTree) {
+        const uint4* g = reinterpret_cast<const uint4*>(a.tree);
+        for (uint32_t k = tid; k < a.tree_lds; k += kBlock) s_tree[k] = g[k];
+    }
     // linear-scan tables past kSmallRules: the IPv6 family list, when the host found room
     // (staging the lists' sorted indexes as well measured slower: config C 41.6 -> 42.7 us)
-    const uint4* s_fam6 = s_fp4;
-    if (kFam && a.fam6_lds) {
+    uint4* s_fam6 = s_fp4 + (kTree ? a.tree_lds : 0u);
+    if (kFamIdx && a.fam6_lds) {
         const uint4* g = a.fam + 2 * (size_t)a.fam4;
-        for (uint32_t k = tid; k < kFamV6Stride * a.fam6; k += kBlock) s_fp4[k] = g[k];
+        for (uint32_t k = tid; k < kFamV6Stride * a.fam6; k += kBlock) s_fam6[k] = g[k];
     }
     const uint16_t* s_fps = kTssMode && a.fp_lds ? reinterpret_cast<const uint16_t*>(s_fp4) : nullptr;
     __syncthreads();
@@ -1618,7 +1739,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         } else {
             // small tables from their LDS copy, larger ones through the scalar unit
             const uint32_t nr = a.nrules_pad;
-            if (kFam)
+            if (kTree)
+                ri = a.tree_lds ? tree_match<true>(a, ok, r.v6, k0, k1, r.s, r.d, act,
+                                                   reinterpret_cast<const uint2*>(s_tree), s_fam6)
+                                : tree_match<false>(a, ok, r.v6, k0, k1, r.s, r.d, act, nullptr, s_fam6);
+            else if (kFam)
                 ri = need_v6 ? scan_fam<true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6)
                              : scan_fam<false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6);
             else if (kGlb)
@@ -1631,7 +1756,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // kFam: ri is the lane's entry in the FamTable index array; the sorted index it holds is
         // loaded now and first used at the verdict store
         uint32_t rsi = ri;
-        if (kFam && ri != kNone)
+        if (kFamIdx && ri != kNone)
             rsi = a.fam_x1idx ? (act >> 18) & 0x1FFFu
                               : reinterpret_cast<const uint32_t*>(a.fam + 2 * (size_t)a.fam4 +
                                                                   (size_t)kFamV6Stride * a.fam6)[ri];
@@ -1646,7 +1771,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             code = UPE_V_DROP_NOMATCH;
         } else {
             const uint32_t ac = (act >> 16) & 3u;
-            if (!kFam) rbits = (ri + 1) << 8;
+            if (!kFamIdx) rbits = (ri + 1) << 8;
             // rule_stats[rule_id] += {1, len}, src/worker.c:141-144: an LDS histogram below for
             // LDS-resident tables; for larger ones upe_rule_hist folds the verdict words after
             // the launch (one scattered device atomic per packet would cost more than the
@@ -1784,7 +1909,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                                                 (a.port_mac_lo >> 16) | (a.port_mac_hi << 16), w[3]));
             if (wrote1) store16(&q[1], make_uint4(w[4], r.c1w1, r.c1w2, w[7]));
         }
-        if (kFam && ok && !r.consumed && ri != kNone) rbits = (rsi + 1) << 8;
+        if (kFamIdx && ok && !r.consumed && ri != kNone) rbits = (rsi + 1) << 8;
         if (live)   // written through (sc1): no dirty lines left for the boundary
             __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -2327,6 +2452,12 @@ struct upe_gpu_ctx {
     // rule it can reach first (up to its family's first catch-all) forwards
     bool fwd4 = true, fwd6 = true;
     uint32_t fam_x1idx = 0;
+    // decision-tree index over the family lists (null / tree_ok false when not used)
+    uint4* tree = nullptr;
+    uint32_t tree_words = 0, tree_loff = 0;
+    bool tree_ok = false;
+    bool tree_stage = true;                    // stage the image in LDS when it fits
+    upe_rule_index_info_t tree_info = {};
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
@@ -2574,14 +2705,15 @@ hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->strea
 constexpr int kVarCount = 256;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
-// upe_gpu_process_host; not ring), bit 6 a linear-scan table past kSmallRules scanned through
-// its family lists (FamTable), bit 7 the same scanned whole (neither with tuple space).
+// upe_gpu_process_host; not ring), bits 6-7 how a linear-scan table past kSmallRules is matched
+// (never with tuple space): 1 its family lists (FamTable), 2 the whole table through the scalar
+// unit, 3 the decision tree over the family lists.
 enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
-       VAR_FAM = 64, VAR_GLB = 128 };
-// scan: 0 small table (LDS copy), 1 family lists, 2 whole table through the scalar unit
+       VAR_FAM = 64, VAR_GLB = 128, VAR_TREE = 192, VAR_SCAN = 192 };
+// scan: 0 small table (LDS copy), 1 family lists, 2 whole table through the scalar unit, 3 tree
 int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
                  int scan = 0) {
-    return (!tss && scan == 1 ? VAR_FAM : 0) | (!tss && scan == 2 ? VAR_GLB : 0) |
+    return (!tss ? (scan & 3) * VAR_FAM : 0) |
            (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) |
            (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
 }
@@ -2590,8 +2722,7 @@ constexpr bool var_built(int v) {
     const bool emit = v & VAR_EMIT, lean = v & VAR_LEAN, nolb = v & VAR_NOLB, ring = v & VAR_RING,
                host = v & VAR_HOST;
     if (nolb && !lean) return false;
-    if ((v & (VAR_FAM | VAR_GLB)) && (v & VAR_TSS)) return false;
-    if ((v & VAR_FAM) && (v & VAR_GLB)) return false;
+    if ((v & VAR_SCAN) && (v & VAR_TSS)) return false;
     if (ring) return !host && emit && lean && !(v & VAR_TSS);
     return true;
 }
@@ -2601,7 +2732,7 @@ const void* classify_fn_of() {
         return reinterpret_cast<const void*>(
             &upe_classify<(V & VAR_TSS) != 0, (V & VAR_EMIT) != 0, (V & VAR_LEAN) != 0,
                           (V & VAR_NOLB) != 0, (V & VAR_RING) != 0, (V & VAR_HOST) != 0,
-                          (V & VAR_FAM) != 0, (V & VAR_GLB) != 0>);
+                          (V & VAR_SCAN) / VAR_FAM>);
     else
         return nullptr;
 }
@@ -2863,7 +2994,7 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     DevScope dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->rv4, c->rv6, c->rinfo, c->stats_idx, c->gb, c->arp, c->ndp, c->st, c->stats,
-                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs, c->fam,
+                    c->pay, c->lb, c->tg4, c->tg6, c->tt4, c->tt6, c->tfs, c->fam, c->tree,
                     c->compact_counts,
                     c->ctrl_marks, c->ctrl_index, c->ctrl_count, c->ctrl_win, c->ctrl_lens,
                     c->hist_part};
@@ -3060,6 +3191,299 @@ bool build_tss_family(int F, const std::vector<RuleV4>& v4, const std::vector<Ru
     return true;
 }
 
+// ---- decision-tree index (round 5; TreeNode comment) ----------------------------------------
+// The conservative range of one rule of a family list on one key word: lo = x & m, hi = x | ~m
+// (within the word's width); `exact` when ~m is a run of low bits (prefix, exact value or
+// wildcard), so that the range is exactly the set of values the rule accepts on that word.
+struct TreeRule {
+    uint32_t lo[kTreeDims], hi[kTreeDims];
+    uint16_t exact;   // bit d: word d's range is exact
+};
+constexpr uint32_t kTreeWidth[kTreeDims] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                            0xFFFFu, 0xFFFFu, 0xFFu};
+// A family list entry (RuleV4 words, plus the IPv6 words for family 6) as key-word ranges.  IPv6
+// address words are compared big-endian (a prefix is then a range); IPv4 word 0 is host order
+// already (src/parser.c:40-41) and its other address words are 0 in the key.
+TreeRule tree_rule(int F, const RuleV4& r, const RuleV6* q) {
+    TreeRule t;
+    uint32_t x[kTreeDims] = {}, m[kTreeDims] = {};
+    if (F == 4) {
+        x[0] = r.s0; m[0] = r.sm0;
+        x[4] = r.d0; m[4] = r.dm0;
+    } else {
+        x[0] = bswap32(r.s0); m[0] = bswap32(r.sm0);
+        x[4] = bswap32(r.d0); m[4] = bswap32(r.dm0);
+        for (int j = 1; j < 4; ++j) {
+            x[j] = bswap32(q->s[j - 1]); m[j] = bswap32(q->sm[j - 1]);
+            x[4 + j] = bswap32(q->d[j - 1]); m[4 + j] = bswap32(q->dm[j - 1]);
+        }
+    }
+    x[8] = r.x0 >> 16; m[8] = r.m0 >> 16;
+    x[9] = r.x1 & 0xFFFFu; m[9] = r.m1 & 0xFFFFu;
+    x[10] = (r.x0 >> 8) & 0xFFu; m[10] = (r.m0 >> 8) & 0xFFu;
+    t.exact = 0;
+    for (int d = 0; d < kTreeDims; ++d) {
+        const uint32_t w = kTreeWidth[d], inv = ~m[d] & w;
+        t.lo[d] = x[d] & m[d] & w;
+        t.hi[d] = (x[d] & w) | inv;
+        if ((inv & (inv + 1u)) == 0) t.exact |= (uint16_t)(1u << d);
+    }
+    return t;
+}
+
+struct TreeImage {
+    std::vector<uint2> nodes;
+    std::vector<uint32_t> leaves;
+    uint32_t trees[2] = {0, 0};      // trees per family
+    uint32_t depth[2] = {0, 0};      // deepest leaf per family
+    uint32_t max_leaf = 0;           // longest leaf list
+};
+
+// HyperSplit-style build of one family's tree into img (breadth first, so the top levels are
+// contiguous).  rules: the family list's entries in list order.  Returns false when the node
+// budget or the leaf-length limit is exceeded (the table then keeps the linear scan).
+bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_t>& members,
+                       int fam_slot, uint32_t binth, size_t node_budget, TreeImage& img) {
+    struct Task {
+        uint32_t node;
+        uint32_t depth;
+        std::array<uint32_t, kTreeDims> lo, hi;
+        std::vector<uint32_t> list;
+    };
+    const uint32_t root = (uint32_t)img.nodes.size();
+    img.nodes.push_back(make_uint2(0, 0));
+    std::deque<Task> q;
+    Task t0;
+    t0.node = root;
+    t0.depth = 0;
+    for (int d = 0; d < kTreeDims; ++d) {
+        t0.lo[d] = 0;
+        t0.hi[d] = kTreeWidth[d];
+    }
+    t0.list = members;
+    q.push_back(std::move(t0));
+    std::vector<uint32_t> los, his, cand;
+    while (!q.empty()) {
+        Task t = std::move(q.front());
+        q.pop_front();
+        // keep the rules up to the first one that matches every key of the box
+        std::vector<uint32_t>& L = t.list;
+        std::vector<uint8_t> covers(L.size(), 0);
+        for (size_t j = 0; j < L.size(); ++j) {
+            const TreeRule& r = R[L[j]];
+            bool cov = true;
+            for (int d = 0; d < kTreeDims && cov; ++d)
+                cov = (r.exact >> d & 1u) && r.lo[d] <= t.lo[d] && r.hi[d] >= t.hi[d];
+            if (cov) {
+                covers[j] = 1;
+                L.resize(j + 1);
+                covers.resize(j + 1);
+                break;
+            }
+        }
+        const uint32_t n = (uint32_t)L.size();
+        int best_d = -1;
+        uint32_t best_t = 0, best_max = n, best_sum = 2 * n;
+        if (n > binth && !covers[0]) {
+            for (int d = 0; d < kTreeDims; ++d) {
+                los.clear();
+                his.clear();
+                bool split = false;
+                for (uint32_t j : L) {
+                    const uint32_t lo = std::max(R[j].lo[d], t.lo[d]);
+                    const uint32_t hi = std::min(R[j].hi[d], t.hi[d]);
+                    los.push_back(lo);
+                    his.push_back(hi);
+                    split |= lo > t.lo[d] || hi < t.hi[d];
+                }
+                if (!split) continue;
+                std::sort(los.begin(), los.end());
+                std::sort(his.begin(), his.end());
+                cand.clear();
+                for (uint32_t v : los)
+                    if (v > t.lo[d]) cand.push_back(v);
+                for (uint32_t v : his)
+                    if (v < t.hi[d]) cand.push_back(v + 1u);
+                std::sort(cand.begin(), cand.end());
+                cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+                size_t il = 0, ih = 0;
+                for (uint32_t c : cand) {
+                    while (il < los.size() && los[il] < c) ++il;   // rules reaching below c
+                    while (ih < his.size() && his[ih] < c) ++ih;   // rules ending below c
+                    const uint32_t nl = (uint32_t)il, nr = n - (uint32_t)ih;
+                    const uint32_t mx = std::max(nl, nr), sm = nl + nr;
+                    if (mx < best_max || (mx == best_max && sm < best_sum)) {
+                        best_max = mx;
+                        best_sum = sm;
+                        best_d = d;
+                        best_t = c;
+                    }
+                }
+            }
+        }
+        if (best_d < 0 || best_max >= n) {
+            // a leaf: its rules in list order, the covering one flagged
+            if (n >= (1u << 11)) return false;
+            img.nodes[t.node] = make_uint2(16u | n << 5, (uint32_t)img.leaves.size());
+            for (uint32_t j = 0; j < n; ++j)
+                img.leaves.push_back(L[j] | (covers[j] ? 0x80000000u : 0u));
+            img.max_leaf = std::max(img.max_leaf, n);
+            img.depth[fam_slot] = std::max(img.depth[fam_slot], t.depth);
+            std::vector<uint32_t>().swap(L);
+            continue;
+        }
+        if (img.nodes.size() + 2 > node_budget || img.nodes.size() + 2 >= (1u << 27)) return false;
+        const uint32_t child = (uint32_t)img.nodes.size();
+        img.nodes.push_back(make_uint2(0, 0));
+        img.nodes.push_back(make_uint2(0, 0));
+        img.nodes[t.node] = make_uint2((uint32_t)best_d | child << 5, best_t);
+        Task a, b;
+        a.node = child;
+        b.node = child + 1;
+        a.depth = b.depth = t.depth + 1;
+        a.lo = b.lo = t.lo;
+        a.hi = b.hi = t.hi;
+        a.hi[best_d] = best_t - 1u;
+        b.lo[best_d] = best_t;
+        for (uint32_t j : L) {
+            if (std::max(R[j].lo[best_d], t.lo[best_d]) < best_t) a.list.push_back(j);
+            if (std::min(R[j].hi[best_d], t.hi[best_d]) >= best_t) b.list.push_back(j);
+        }
+        std::vector<uint32_t>().swap(L);
+        q.push_back(std::move(a));
+        q.push_back(std::move(b));
+    }
+    return true;
+}
+
+// One family's forest: its rules grouped by the key word on which each overlaps the fewest
+// other rules of the list (EffiCuts-style separation: a rule narrow only in its destination port
+// is not copied into every leaf of a tree that splits on addresses), one tree per group, every
+// tree's rules in list order.  A key's first match is the smallest of its first matches in the
+// trees (the groups partition the list).  A rule that matches every key of the family (the list's
+// last entry, if any) gets a one-leaf tree of its own.
+bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
+                         size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots) {
+    const size_t n = R.size();
+    roots.clear();
+    if (n == 0) return true;
+    std::vector<int> grp(n, -1);
+    std::vector<uint32_t> best(n, 0xFFFFFFFFu);
+    std::vector<uint32_t> los(n), his(n);
+    for (int d = 0; d < kTreeDims; ++d) {
+        for (size_t i = 0; i < n; ++i) {
+            los[i] = R[i].lo[d];
+            his[i] = R[i].hi[d];
+        }
+        std::sort(los.begin(), los.end());
+        std::sort(his.begin(), his.end());
+        for (size_t i = 0; i < n; ++i) {
+            // rules whose range meets rule i's on word d: lo <= hi_i, minus those ending below lo_i
+            const size_t a = (size_t)(std::upper_bound(los.begin(), los.end(), R[i].hi[d]) - los.begin());
+            const size_t b = (size_t)(std::lower_bound(his.begin(), his.end(), R[i].lo[d]) - his.begin());
+            const uint32_t ov = (uint32_t)(a - b);
+            if (ov < best[i]) {
+                best[i] = ov;
+                grp[i] = d;
+            }
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        bool all = true;
+        for (int d = 0; d < kTreeDims && all; ++d)
+            all = (R[i].exact >> d & 1u) && R[i].lo[d] == 0 && R[i].hi[d] == kTreeWidth[d];
+        if (all) grp[i] = kTreeDims;   // matches every key of the family
+    }
+    for (int g = 0; g <= kTreeDims; ++g) {
+        std::vector<uint32_t> members;
+        for (size_t i = 0; i < n; ++i)
+            if (grp[i] == g) members.push_back((uint32_t)i);
+        if (members.empty()) continue;
+        roots.push_back((uint32_t)img.nodes.size());
+        const size_t n0 = img.nodes.size(), e0 = img.leaves.size();
+        // (large groups: longer leaves, or nested prefixes multiply the leaves)
+        const uint32_t bt = members.size() > 4096 ? std::max(binth, 16u) : binth;
+        const bool ok = build_tree_family(R, members, fam_slot, bt, node_budget, img);
+        if (getenv("UPE_GPU_VERBOSE"))
+            fprintf(stderr, "upe_gpu: tree family %d group %d: %zu rules, %zu nodes, %zu leaf entries%s\n",
+                    fam_slot ? 6 : 4, g, members.size(), img.nodes.size() - n0,
+                    img.leaves.size() - e0, ok ? "" : " (over budget)");
+        if (!ok) return false;
+    }
+    return true;
+}
+
+// The forests of both family lists (l4 / l6: sorted indexes of the list entries), after a
+// directory: node 0 = {trees of family 4, trees of family 6}, then a copy of each tree's root
+// (family 4's trees first), so that a walk starts without an indirection.
+bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, uint32_t binth,
+                size_t node_budget, TreeImage& img) {
+    img = TreeImage();
+    TreeImage body;
+    std::vector<TreeRule> R;
+    std::vector<uint32_t> r4, r6;
+    for (uint32_t i : l4) R.push_back(tree_rule(4, v4[i], nullptr));
+    if (!build_forest_family(R, 0, binth, node_budget, body, r4)) return false;
+    R.clear();
+    for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i]));
+    if (!build_forest_family(R, 1, binth, node_budget, body, r6)) return false;
+    const uint32_t dir = 1u + (uint32_t)(r4.size() + r6.size());
+    auto shift = [&](uint2 nd) {   // inner nodes' child indexes move by the directory's size
+        return (nd.x & 16u) ? nd : make_uint2((nd.x & 15u) | (((nd.x >> 5) + dir) << 5), nd.y);
+    };
+    img.nodes.push_back(make_uint2((uint32_t)r4.size(), (uint32_t)r6.size()));
+    for (uint32_t r : r4) img.nodes.push_back(shift(body.nodes[r]));
+    for (uint32_t r : r6) img.nodes.push_back(shift(body.nodes[r]));
+    for (uint2 nd : body.nodes) img.nodes.push_back(shift(nd));
+    img.leaves = std::move(body.leaves);
+    img.depth[0] = body.depth[0];
+    img.depth[1] = body.depth[1];
+    img.max_leaf = body.max_leaf;
+    img.trees[0] = (uint32_t)r4.size();
+    img.trees[1] = (uint32_t)r6.size();
+    return img.nodes.size() < (1u << 27);
+}
+
+// Host walk of the image, bit for bit what tree_match does on the device: the list position of
+// the key's first match (kNone = none).  kv: the key words (kTreeDims comment).
+uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
+                        const std::vector<RuleV6>& v6, const std::vector<uint32_t>& list, bool is6,
+                        const uint32_t kv[kTreeDims], uint32_t k0, uint32_t k1, const uint32_t s[4],
+                        const uint32_t d[4]) {
+    const uint2 dir = img.nodes[0];
+    const uint32_t nt = is6 ? dir.y : dir.x, first = 1u + (is6 ? dir.x : 0u);
+    uint32_t best = kNone;
+    for (uint32_t t = 0; t < nt; ++t) {
+        uint2 nd = img.nodes[first + t];
+        while (!(nd.x & 16u)) nd = img.nodes[(nd.x >> 5) + (kv[nd.x & 15u] >= nd.y ? 1u : 0u)];
+        const uint32_t cnt = nd.x >> 5;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t e = img.leaves[nd.y + j];
+            const uint32_t pos = e & 0x7FFFFFFFu;
+            if (pos >= best) break;
+            bool hit = (e >> 31) != 0;
+            if (!hit) {
+                const RuleV4& r = v4[list[pos]];
+                uint32_t x = ((k0 ^ r.x0) & r.m0) | ((k1 ^ r.x1) & r.m1 & 0xFFFFu) |
+                             ((s[0] ^ r.s0) & r.sm0) | ((d[0] ^ r.d0) & r.dm0);
+                if (is6) {
+                    const RuleV6& q6 = v6[list[pos]];
+                    for (int w = 0; w < 3; ++w)
+                        x |= ((s[w + 1] ^ q6.s[w]) & q6.sm[w]) | ((d[w + 1] ^ q6.d[w]) & q6.dm[w]);
+                }
+                hit = x == 0;
+            }
+            if (hit) {
+                best = pos;
+                break;
+            }
+        }
+    }
+    return best;
+}
+
 int upload_bytes(void** dst, const void* src, size_t bytes) {
     if (*dst) (void)hipFree(*dst);
     *dst = nullptr;
@@ -3077,18 +3501,13 @@ int upload(uint4*& dst, const std::vector<uint4>& v) {
 int upload(uint16_t*& dst, const std::vector<uint16_t>& v) {
     return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint16_t));
 }
-}  // namespace
-extern "C" {
-
-extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count) {
-    if (!c) return fail("null context");
-    if (count > c->cap) return fail("rule count exceeds the capacity given at open");
-    if (count && !rules) return fail("null rules");
-    DEV_SCOPE(c->device);
-    const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
-    std::vector<RuleV4> v4(pad);
-    std::vector<RuleV6> v6(pad);
-    std::vector<int2> info(pad);
+// rule_t -> the compiled words: RuleV4 / RuleV6 (pre-masked) and rinfo, pad >= count entries (the
+// padding never matches).  -1 (message set) on a rule_id outside [0, cap).
+int compile_rules(const upe_rule_t* rules, size_t count, size_t cap, size_t pad,
+                  std::vector<RuleV4>& v4, std::vector<RuleV6>& v6, std::vector<int2>& info) {
+    v4.assign(pad, RuleV4{});
+    v6.assign(pad, RuleV6{});
+    info.assign(pad, make_int2(0, 0));
     for (size_t i = 0; i < pad; ++i) {
         RuleV4& a = v4[i];
         RuleV6& b = v6[i];
@@ -3098,11 +3517,10 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             // never matches: ip_ver byte 0xFF against a key version of 4 or 6
             a.x0 = 0xFF;
             a.m0 = 0xFF;
-            info[i] = make_int2(0, 0);
             continue;
         }
         const upe_rule_t& r = rules[i];
-        if (r.rule_id >= c->cap) return fail("rule_id >= capacity (rule_stats index)");
+        if (r.rule_id >= cap) return fail("rule_id >= capacity (rule_stats index)");
         a.x0 = (uint32_t)r.ip_ver | ((uint32_t)r.protocol << 8) | ((uint32_t)r.src_port << 16);
         a.m0 = (r.ip_ver ? 0xFFu : 0u) | (r.protocol ? 0xFF00u : 0u) |
                (r.src_port ? 0xFFFF0000u : 0u);
@@ -3127,6 +3545,59 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         if (v6w) a.m1 |= kRuleV6Words;   // IPv6 keys must test this rule's rv6 words
         info[i] = make_int2(r.action.type, (int)r.rule_id);
     }
+    return 0;
+}
+
+// Does compiled rule i match every key of family 4 / 6?
+bool matches_all4(const RuleV4& e) {
+    return (e.m0 & 0xFFFFFF00u) == 0 && (e.m1 & 0xFFFFu) == 0 && e.sm0 == 0 && e.dm0 == 0;
+}
+bool matches_all6(const RuleV4& e, const RuleV6& q) {
+    bool all = matches_all4(e);
+    for (int j = 0; j < 3; ++j) all = all && q.sm[j] == 0 && q.dm[j] == 0;
+    return all;
+}
+
+// The family lists (FamTable): the sorted indexes of the rules a key of each family can match
+// (ip_ver 4 or 0, 6 or 0), each ending at its family's first rule that matches every key of the
+// family (nothing after it can be a first match: seed-3 config C's IPv6 list is one entry long).
+void family_lists(const upe_rule_t* rules, size_t count, const std::vector<RuleV4>& v4,
+                  const std::vector<RuleV6>& v6, std::vector<uint32_t>& l4,
+                  std::vector<uint32_t>& l6, bool& end4, bool& end6) {
+    l4.clear();
+    l6.clear();
+    end4 = end6 = false;
+    for (size_t i = 0; i < count; ++i) {
+        const uint8_t ver = rules[i].ip_ver;
+        if (!end4 && (ver == 0 || ver == 4)) {
+            l4.push_back((uint32_t)i);
+            end4 = matches_all4(v4[i]);
+        }
+        if (!end6 && (ver == 0 || ver == 6)) {
+            l6.push_back((uint32_t)i);
+            end6 = matches_all6(v4[i], v6[i]);
+        }
+    }
+}
+
+size_t tree_node_budget(size_t count) {
+    const char* e = getenv("UPE_GPU_TREE_BUDGET");   // diagnostic override
+    if (e) return (size_t)strtoull(e, nullptr, 10);
+    return std::max<size_t>(1u << 16, 64 * count);
+}
+}  // namespace
+extern "C" {
+
+extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count) {
+    if (!c) return fail("null context");
+    if (count > c->cap) return fail("rule count exceeds the capacity given at open");
+    if (count && !rules) return fail("null rules");
+    DEV_SCOPE(c->device);
+    const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
+    std::vector<RuleV4> v4;
+    std::vector<RuleV6> v6;
+    std::vector<int2> info;
+    if (compile_rules(rules, count, c->cap, pad, v4, v6, info) != 0) return -1;
     // previous batches may still read the table, on whichever stream they went
     if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3158,11 +3629,7 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
         c->fwd4 = c->fwd6 = false;
         for (size_t i = 0; i < count && !(e4 && e6); ++i) {
             const uint8_t ver = rules[i].ip_ver;
-            const RuleV4& e = v4[i];
-            const bool all4 = (e.m0 & 0xFFFFFF00u) == 0 && (e.m1 & 0xFFFFu) == 0 && e.sm0 == 0 &&
-                              e.dm0 == 0;
-            bool all6 = all4;
-            for (int j = 0; j < 3; ++j) all6 = all6 && v6[i].sm[j] == 0 && v6[i].dm[j] == 0;
+            const bool all4 = matches_all4(v4[i]), all6 = matches_all6(v4[i], v6[i]);
             const bool fwd = rules[i].action.type == UPE_ACT_FWD;
             if (!e4 && (ver == 0 || ver == 4)) { c->fwd4 = c->fwd4 || fwd; e4 = all4; }
             if (!e6 && (ver == 0 || ver == 6)) { c->fwd6 = c->fwd6 || fwd; e6 = all6; }
@@ -3175,27 +3642,10 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
     c->fam4 = c->fam6 = 0;
     c->fam_all = 0;
     c->fam_x1idx = 0;
+    std::vector<uint32_t> l4, l6;   // the family lists' sorted indexes
     if (pad > (size_t)kSmallRules) {
-        // each list ends at its first rule that matches every key of its family (nothing after
-        // it can be a first match: config C's IPv6 list is one entry long)
-        std::vector<uint32_t> l4, l6;
         bool end4 = false, end6 = false;
-        for (size_t i = 0; i < count; ++i) {
-            const uint8_t ver = rules[i].ip_ver;
-            const RuleV4& e = v4[i];
-            const bool all4 = (e.m0 & 0xFFFFFF00u) == 0 && (e.m1 & 0xFFFFu) == 0 && e.sm0 == 0 &&
-                              e.dm0 == 0;
-            bool all6 = all4;
-            for (int j = 0; j < 3; ++j) all6 = all6 && v6[i].sm[j] == 0 && v6[i].dm[j] == 0;
-            if (!end4 && (ver == 0 || ver == 4)) {
-                l4.push_back((uint32_t)i);
-                end4 = all4;
-            }
-            if (!end6 && (ver == 0 || ver == 6)) {
-                l6.push_back((uint32_t)i);
-                end6 = all6;
-            }
-        }
+        family_lists(rules, count, v4, v6, l4, l6, end4, end6);
         const size_t n4 = (l4.size() + kUnroll - 1) / kUnroll * kUnroll;
         const size_t n6 = (l6.size() + kUnroll - 1) / kUnroll * kUnroll;
         // (+1: the scalar scan loads an IPv6 entry's last 48 bytes as 64)
@@ -3281,6 +3731,31 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             }
         }
     }
+    // Linear-scan tables past kSmallRules without a tuple-space index: the decision tree over the
+    // family lists (kTreeDims comment), unless it outgrows its node budget (UPE_GPU_TREE: 0 = never,
+    // diagnostic; UPE_GPU_TREE_BINTH: rules per leaf before a split)
+    c->tree_ok = false;
+    const char* tf = getenv("UPE_GPU_TREE");
+    const char* tl = getenv("UPE_GPU_TREE_LDS");   // diagnostic: 0 = the image stays in memory
+    c->tree_stage = !(tl && tl[0] == '0');
+    if (!c->tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0')) {
+        const char* bt = getenv("UPE_GPU_TREE_BINTH");
+        const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : kTreeBinth;
+        TreeImage t;
+        if (build_tree(v4, v6, l4, l6, binth, tree_node_budget(count), t)) {
+            const size_t nw = 2 * t.nodes.size() + t.leaves.size();
+            std::vector<uint4> img((nw + 3) / 4, make_uint4(0, 0, 0, 0));
+            memcpy(img.data(), t.nodes.data(), t.nodes.size() * sizeof(uint2));
+            memcpy(reinterpret_cast<uint32_t*>(img.data()) + 2 * t.nodes.size(), t.leaves.data(),
+                   t.leaves.size() * sizeof(uint32_t));
+            if (upload(c->tree, img)) return -1;
+            c->tree_words = (uint32_t)img.size();
+            c->tree_loff = (uint32_t)(2 * t.nodes.size());
+            c->tree_info = {(uint64_t)t.nodes.size(), (uint64_t)t.leaves.size(), t.depth[0],
+                            t.depth[1], t.max_leaf, t.trees[0] | t.trees[1] << 16};
+            c->tree_ok = true;
+        }
+    }
     return 0;
 }
 
@@ -3327,7 +3802,85 @@ extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, s
 
 extern "C" int upe_gpu_rule_index_kind(upe_gpu_ctx_t* c) {
     if (!c) return fail("null context");
-    return c->tss ? 1 : 0;
+    return c->tss ? 1 : c->tree_ok ? 2 : 0;
+}
+
+extern "C" int upe_gpu_rule_index_info(upe_gpu_ctx_t* c, upe_rule_index_info_t* info) {
+    if (!c || !info) return fail("null argument");
+    *info = c->tree_ok ? c->tree_info : upe_rule_index_info_t{};
+    return 0;
+}
+
+// rule_table_match (reference src/rule_table.c:163-176) for a batch of keys on the host, through
+// the decision tree the GPU path builds for the same table (tree_walk_host: the device's walk bit
+// for bit), or the family lists' linear first match when the table gets no tree.
+extern "C" int upe_rules_match_host(const upe_rule_t* rules, size_t count,
+                                    const upe_flow_key_t* keys, size_t n, int64_t* out,
+                                    upe_rule_index_info_t* info) {
+    if ((count && !rules) || (n && (!keys || !out))) return fail("null argument");
+    const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;
+    std::vector<RuleV4> v4;
+    std::vector<RuleV6> v6;
+    std::vector<int2> rinfo;
+    if (compile_rules(rules, count, 0xFFFFFFFFu, pad, v4, v6, rinfo) != 0) return -1;
+    std::vector<uint32_t> l4, l6;
+    bool end4 = false, end6 = false;
+    family_lists(rules, count, v4, v6, l4, l6, end4, end6);
+    const char* bt = getenv("UPE_GPU_TREE_BINTH");
+    const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : kTreeBinth;
+    TreeImage t;
+    const bool tree = build_tree(v4, v6, l4, l6, binth, tree_node_budget(count), t);
+    if (info)
+        *info = tree ? upe_rule_index_info_t{(uint64_t)t.nodes.size(), (uint64_t)t.leaves.size(),
+                                             t.depth[0], t.depth[1], t.max_leaf,
+                                             t.trees[0] | t.trees[1] << 16}
+                     : upe_rule_index_info_t{};
+    for (size_t i = 0; i < n; ++i) {
+        const upe_flow_key_t& k = keys[i];
+        if (k.ip_ver != 4 && k.ip_ver != 6) {
+            out[i] = -1;
+            continue;
+        }
+        const bool is6 = k.ip_ver == 6;
+        const uint32_t k0 = (uint32_t)k.ip_ver | ((uint32_t)k.protocol << 8) |
+                            ((uint32_t)k.src_port << 16);
+        const uint32_t k1 = k.dst_port;
+        uint32_t sw[4], dw[4], kv[kTreeDims] = {};
+        for (int j = 0; j < 4; ++j) {
+            sw[j] = le32(k.src_ip.v6 + 4 * j);
+            dw[j] = le32(k.dst_ip.v6 + 4 * j);
+        }
+        if (is6) {
+            for (int j = 0; j < 4; ++j) {
+                kv[j] = bswap32(sw[j]);
+                kv[4 + j] = bswap32(dw[j]);
+            }
+        } else {
+            kv[0] = sw[0];
+            kv[4] = dw[0];
+        }
+        kv[8] = k.src_port;
+        kv[9] = k.dst_port;
+        kv[10] = k.protocol;
+        const std::vector<uint32_t>& list = is6 ? l6 : l4;
+        uint32_t pos = kNone;
+        if (tree) {
+            pos = tree_walk_host(t, v4, v6, list, is6, kv, k0, k1, sw, dw);
+        } else {
+            for (size_t j = 0; j < list.size() && pos == kNone; ++j) {
+                const RuleV4& r = v4[list[j]];
+                uint32_t x = ((k0 ^ r.x0) & r.m0) | ((k1 ^ r.x1) & r.m1 & 0xFFFFu) |
+                             ((sw[0] ^ r.s0) & r.sm0) | ((dw[0] ^ r.d0) & r.dm0);
+                if (is6)
+                    for (int w = 0; w < 3; ++w)
+                        x |= ((sw[w + 1] ^ v6[list[j]].s[w]) & v6[list[j]].sm[w]) |
+                             ((dw[w + 1] ^ v6[list[j]].d[w]) & v6[list[j]].dm[w]);
+                if (x == 0) pos = (uint32_t)j;
+            }
+        }
+        out[i] = pos == kNone ? -1 : (int64_t)list[pos];
+    }
+    return 0;
 }
 
 int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_capacity,
@@ -3529,6 +4082,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.fam4 = c->fam4;
     a.fam6 = c->fam6;
     a.fam_x1idx = c->fam_x1idx;
+    a.tree = reinterpret_cast<const uint2*>(c->tree);
+    a.tree_loff = c->tree_loff;
     a.rinfo = c->rinfo;
     a.nrules_pad = c->nrules_pad;
     a.arp = arp_index(c);
@@ -3593,8 +4148,19 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         a.fp_lds = c->nfs;
         lds += c->nfs * sizeof(uint4);
     }
+    // large linear tables: the decision tree (when built), else family lists, unless a family's
+    // list is a single catch-all (then the split gains that family nothing and measured slower
+    // for the other)
+    const int scan = c->tss || c->nrules_pad <= (uint32_t)kSmallRules ? 0
+                   : c->tree_ok ? 3 : c->fam_all ? 2 : 1;
+    // the tree's image in LDS first (every lane reads a node per level), then the IPv6 list
+    a.tree_lds = 0u;
+    if (scan == 3 && c->tree_stage && lds + c->tree_words * sizeof(uint4) <= kLdsDynMax) {
+        a.tree_lds = c->tree_words;
+        lds += c->tree_words * sizeof(uint4);
+    }
     a.fam6_lds = 0u;
-    if (kFamLds && !c->tss && !c->fam_all && c->fam6 &&
+    if (kFamLds && !c->tss && (scan == 3 || !c->fam_all) && c->fam6 &&
         lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
         a.fam6_lds = 1u;
         lds += kFamV6Stride * c->fam6 * sizeof(uint4);
@@ -3619,9 +4185,6 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     // (at most kRingMax batches: one LDS counter each)
     bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
-    // large linear tables: family lists, unless a family's list is a single catch-all (then the
-    // split gains that family nothing and measured slower for the other)
-    const int scan = c->tss || c->nrules_pad <= (uint32_t)kSmallRules ? 0 : c->fam_all ? 2 : 1;
     int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, scan);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);

@@ -16,8 +16,9 @@ import os
 
 import numpy as np
 
-from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, L1_DTYPE, LAUNCH_INFO_DTYPE,
-                     NDP_DTYPE, RULE_DTYPE, RULE_STAT_DTYPE)
+from .layout import (ARP_DTYPE, BATCH_INFO_DTYPE, COUNTERS_DTYPE, FLOW_KEY_DTYPE, L1_DTYPE,
+                     LAUNCH_INFO_DTYPE, NDP_DTYPE, RULE_DTYPE, RULE_INDEX_INFO_DTYPE,
+                     RULE_STAT_DTYPE)
 
 LIB_PATH = os.environ.get("UPE_GPU_LIB_DIAG") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "libupe_gpu.so")  # override: diagnostic builds only
@@ -29,6 +30,8 @@ VAR_RING = 16   # a ring launch whose batches are stamped
 VAR_HOST = 32   # a host path's launch (mapped host memory, host round trip)
 VAR_FAM = 64    # a linear-scan table past 64 rules, scanned through per-family rule lists
 VAR_GLB = 128   # the same scanned whole (a family's list is a single catch-all)
+VAR_TREE = 192  # the same matched through the decision tree over the family lists
+VAR_SCAN = 192  # the bits of the three above
 
 
 # upe_tx_batch_fn: int (*)(void *user, const uint8_t *const *frames, const size_t *lens, int count)
@@ -94,6 +97,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_reload_rules": (I, [P, P, SZ, SZ, P, SZ]),
         "upe_gpu_load_neigh": (I, [P, P, SZ, P, SZ]),
         "upe_gpu_rule_index_kind": (I, [P]),
+        "upe_gpu_rule_index_info": (I, [P, P]),
         "upe_gpu_set_port": (I, [P, P, ctypes.c_uint32]),
         "upe_gpu_set_l1": (I, [P, P]),
         "upe_gpu_get_l1": (I, [P, P]),
@@ -133,6 +137,7 @@ def _load() -> ctypes.CDLL:
     }
     sig.update({
         "upe_rules_load_ini": (I, [ctypes.c_char_p, P, SZ, P]),
+        "upe_rules_match_host": (I, [P, SZ, P, SZ, P, P]),
         "upe_pcap_read": (I, [ctypes.c_char_p, P, SZ, P, SZ, P]),
         "upe_host_last_error": (ctypes.c_char_p, []),
     })
@@ -150,8 +155,9 @@ LIB = _load()
 # every symbol include/upe_gpu.h declares (checked by tests/test_abi.py)
 EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", "upe_gpu_pin_self",
             "upe_gpu_open", "upe_gpu_close",
-            "upe_gpu_load_rules", "upe_gpu_reload_rules", "upe_gpu_load_neigh", "upe_gpu_rule_index_kind", "upe_gpu_set_port", "upe_gpu_set_l1",
-            "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
+            "upe_gpu_load_rules", "upe_gpu_reload_rules", "upe_gpu_load_neigh",
+            "upe_gpu_rule_index_kind", "upe_gpu_rule_index_info", "upe_gpu_set_port",
+            "upe_gpu_set_l1", "upe_gpu_get_l1", "upe_gpu_process", "upe_gpu_sync", "upe_gpu_batch_info",
             "upe_gpu_launch_info",
             "upe_gpu_get_stats", "upe_gpu_reset_stats", "upe_gpu_timing_enable",
             "upe_gpu_timing_span",
@@ -162,7 +168,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_gpu_process_segmented", "upe_gpu_process_emit", "upe_gpu_process_batches_emit",
             "upe_gpu_process_ring_emit", "upe_gpu_process_queue_emit",
             "upe_hdr_apply",
-            "upe_rules_load_ini", "upe_pcap_read",
+            "upe_rules_load_ini", "upe_rules_match_host", "upe_pcap_read",
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
@@ -260,11 +266,16 @@ class GpuWorker:
         return old
 
     def rule_index_kind(self) -> int:
-        """0: linear scan, 1: tuple-space index."""
+        """0: linear scan, 1: tuple-space index, 2: decision tree."""
         k = LIB.upe_gpu_rule_index_kind(self._ctx)
         if k < 0:
             raise UpeGpuError(LIB.upe_gpu_last_error().decode())
         return k
+
+    def rule_index_info(self) -> np.ndarray:
+        out = np.zeros(1, RULE_INDEX_INFO_DTYPE)
+        _check(LIB.upe_gpu_rule_index_info(self._ctx, _np_ptr(out)), "upe_gpu_rule_index_info")
+        return out[0]
 
     def load_neigh(self, arp: np.ndarray | None, ndp: np.ndarray | None) -> None:
         a = np.ascontiguousarray(arp if arp is not None else np.zeros(0, ARP_DTYPE), ARP_DTYPE)
@@ -491,6 +502,21 @@ def rules_load_ini(path: str, capacity: int = 1024) -> np.ndarray:
     if rc != 0:
         raise UpeGpuError(LIB.upe_host_last_error().decode())
     return out[: int(count[0])].copy()
+
+
+def rules_match_host(rules_sorted: np.ndarray, keys: np.ndarray):
+    """upe_rules_match_host: the first match of each key (FLOW_KEY_DTYPE) through the decision
+    tree the GPU path builds for the table, walked on the host.  Returns (sorted index or -1 per
+    key, the tree's RULE_INDEX_INFO_DTYPE record; all zero when the table gets no tree)."""
+    r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
+    k = np.ascontiguousarray(keys, dtype=FLOW_KEY_DTYPE)
+    out = np.zeros(len(k), np.int64)
+    info = np.zeros(1, RULE_INDEX_INFO_DTYPE)
+    _check(LIB.upe_rules_match_host(_np_ptr(r) if len(r) else None, len(r),
+                                    _np_ptr(k) if len(k) else None, len(k),
+                                    _np_ptr(out) if len(k) else None, _np_ptr(info)),
+           "upe_rules_match_host")
+    return out, info[0]
 
 
 def pcap_read(path: str):

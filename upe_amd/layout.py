@@ -59,6 +59,15 @@ LAUNCH_INFO_DTYPE = np.dtype({"names": ["variant", "grid", "deferred", "launches
                               "formats": ["<u4", "<u4", "<u4", "<u8"],
                               "offsets": [0, 4, 8, 16], "itemsize": 24})
 
+# flow_key_t (reference include/parser.h:134-141; upe_flow_key_t, 44 bytes)
+FLOW_KEY_DTYPE = np.dtype({"names": ["ip_ver", "src_ip", "dst_ip", "src_port", "dst_port",
+                                     "protocol"],
+                           "formats": ["u1", ("u1", 16), ("u1", 16), "<u2", "<u2", "u1"],
+                           "offsets": [0, 4, 20, 36, 38, 40], "itemsize": 44})
+# upe_rule_index_info_t (include/upe_gpu.h)
+RULE_INDEX_INFO_DTYPE = np.dtype([("nodes", "<u8"), ("leaf_entries", "<u8"), ("depth4", "<u4"),
+                                  ("depth6", "<u4"), ("max_leaf", "<u4"), ("trees", "<u4")])
+
 # verdict word (include/upe_gpu.h)
 V_DROP_PARSE, V_DROP_NOMATCH, V_DROP_RULE, V_DROP_TTL, V_FWD, V_CONSUMED, V_DROP_ACTION = range(7)
 VERDICT_NAMES = ("DROP_PARSE", "DROP_NOMATCH", "DROP_RULE", "DROP_TTL", "FWD", "CONSUMED",

@@ -512,6 +512,194 @@ def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024,
 
 
 # ---------------------------------------------------------------------------------------------
+# config C, flow-derived (round 5): the same IMIX traffic mix and rule shape as config_c, but every
+# rule is cut from a flow of the traffic and kept selective, so that first-match positions spread
+# over the whole 1k table for BOTH families (seed-3 config_c stops every IPv4 packet at sorted
+# rule 11 and every IPv6 packet at rule 0, a priority-1 IPv6 wildcard DROP)
+# ---------------------------------------------------------------------------------------------
+
+V4_SRC_BASE = 0x0A000000     # IPv4 sources: 10.0.0.0/8
+V4_DST_BASE = 0xAC100000     # IPv4 destinations: a pool of hosts in 172.16.0.0/12
+V6_SRC_PRE = bytes.fromhex("20010db8")
+V6_DST_PRE = bytes.fromhex("2001db80")
+C_PROTO4 = (np.array([17, 6, 1]), np.array([0.5, 0.4, 0.1]))
+C_PROTO6 = (np.array([17, 6]), np.array([0.5, 0.5]))
+
+
+def _v6_mask_arr(prefix: int) -> np.ndarray:
+    return np.frombuffer(ipv6_mask(prefix), np.uint8)
+
+
+def _flow_rules(rng, n_rules, dst4, dst6, ports, max_cover):
+    """Rules 0..n_rules-2 (the catch-all is appended by the caller), each cut from a random flow:
+    prefixes /8-/32 (IPv4) and /32-/128 (IPv6) or wildcards, protocol and ports exact or 0, 50/50
+    FWD / DROP, 5 % version-agnostic.  A draw whose estimated share of its family's traffic
+    exceeds max_cover is tightened (a longer prefix, or one more exact field) until it does not,
+    so that no rule covers the traffic pool: a packet cut from rule j's flow first matches rule j
+    (or, rarely, an earlier rule that happens to cover it)."""
+    specs = []
+    prios = rng.permutation(n_rules - 1) + 1
+    for i in range(n_rules - 1):
+        fam = 6 if rng.random() < 0.3 else 4
+        agnostic = rng.random() < 0.05
+        if fam == 4:
+            src = V4_SRC_BASE | int(rng.integers(0, 1 << 24))
+            di = int(rng.integers(len(dst4)))
+            proto = int(rng.choice(C_PROTO4[0], p=C_PROTO4[1]))
+            lo_len, hi_len = 8, 32
+        else:
+            src = V6_SRC_PRE + bytes(rng.integers(0, 256, size=12, dtype=np.uint8))
+            di = int(rng.integers(len(dst6)))
+            proto = int(rng.choice(C_PROTO6[0], p=C_PROTO6[1]))
+            lo_len, hi_len = 32, 128
+        ls = int(rng.integers(lo_len, hi_len + 1)) if rng.random() < 0.7 else None
+        ld = int(rng.integers(lo_len, hi_len + 1)) if rng.random() < 0.7 else None
+        has = {"proto": rng.random() < 0.5, "sport": rng.random() < 0.3,
+               "dport": rng.random() < 0.4}
+        if agnostic and rng.random() < 0.5:
+            ls = ld = None   # ports / protocol only: the rule applies to both families
+        sport = int(ports[rng.integers(len(ports))])
+        dport = int(ports[rng.integers(len(ports))])
+
+        def dst_pool_in(l):
+            if l is None:
+                return None
+            if fam == 4:
+                m = ipv4_mask(l)
+                return np.nonzero((dst4.astype(np.uint64) & m) == (int(dst4[di]) & m))[0]
+            m = _v6_mask_arr(l)
+            return np.nonzero(np.all((dst6 & m) == (dst6[di] & m), axis=1))[0]
+
+        def cover():
+            c = 1.0
+            if ls is not None:
+                c *= 2.0 ** -(max(ls, lo_len) - lo_len)
+            if ld is not None:
+                c *= len(dst_pool_in(ld)) / (len(dst4) if fam == 4 else len(dst6))
+            if has["proto"]:
+                tab = C_PROTO4 if fam == 4 else C_PROTO6
+                c *= float(tab[1][list(tab[0]).index(proto)])
+            c *= (1.0 / len(ports)) ** (int(has["sport"]) + int(has["dport"]))
+            return c
+
+        tries = 0
+        while cover() > max_cover:
+            k = int(rng.integers(0, 5))
+            tries += 1
+            # (a ports-only version-agnostic rule gets an address too once its ports and
+            # protocol alone cannot reach max_cover)
+            if k == 0 and not (agnostic and ls is None and tries < 16):
+                ls = lo_len if ls is None else min(hi_len, ls + 4)
+            elif k == 1 and not (agnostic and ld is None and tries < 16):
+                ld = lo_len if ld is None else min(hi_len, ld + 4)
+            elif k == 2:
+                has["proto"] = True
+            elif k == 3:
+                has["sport"] = True
+            elif k == 4:
+                has["dport"] = True
+        specs.append(dict(fam=fam, ver=0 if agnostic else fam, src=src, ls=ls, di=di, ld=ld,
+                          proto=proto if has["proto"] else 0,
+                          sport=sport if has["sport"] else 0,
+                          dport=dport if has["dport"] else 0,
+                          act=ACT_FWD if rng.random() < 0.5 else ACT_DROP,
+                          prio=int(prios[i]), pool=dst_pool_in(ld)))
+    rules = []
+    for s in specs:
+        dst = (int(dst4[s["di"]]) if s["fam"] == 4 else bytes(dst6[s["di"]]))
+        rules.append(make_rule(s["prio"], s["act"], ip_ver=s["ver"], proto=s["proto"],
+                               sport=s["sport"], dport=s["dport"],
+                               src=None if s["ls"] is None else (s["src"], s["ls"]),
+                               dst=None if s["ld"] is None else (dst, s["ld"])))
+    rules.append(make_rule(1 << 30, ACT_DROP))
+    return specs, rules_array(rules)
+
+
+def config_c_flows(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024,
+                   max_cover: float = 2.0 ** -14, stray: float = 0.05) -> Workload:
+    """BASELINE configs[2] with first-match positions spread over the table (the bench's `imix`
+    leg from round 5; `config_c` seed 3 is kept as `imix_seed3`).  Traffic as SURVEY.md §8(d)
+    row C: IMIX 64/570/1518 (7:4:1; a frame is never shorter than its headers), 70 % IPv4 (UDP 50 /
+    TCP 40 / ICMP 10 %), 30 % IPv6 (UDP / TCP); 1k rules (`_flow_rules`) + the catch-all; ARP and
+    NDP hold 600 of the 1000 destination hosts of each family.  Each packet is cut from a random
+    rule's flow (fields the rule constrains by prefix randomised inside the prefix, the
+    destination drawn from the pool hosts inside it; wildcard fields drawn from the traffic's
+    distributions), except `stray` of them drawn with no rule in mind (the catch-all, after a
+    scan of the whole table)."""
+    rng = np.random.default_rng(seed + 7000)
+    n_hosts = 1000
+    dst4 = (V4_DST_BASE + rng.choice(1 << 20, size=n_hosts, replace=False)).astype(np.uint64)
+    dst6 = _v6_pool(rng, n_hosts, prefix=V6_DST_PRE)
+    ports = np.concatenate([np.array([53, 80, 443, 22, 123, 8080]),
+                            rng.integers(1024, 65536, size=200)])
+    arp = arp_table(1024, [(int(ip), _rand_macs(rng, 1)[0].tobytes())
+                           for ip in dst4[rng.permutation(n_hosts)[:600]]])
+    ndp = ndp_table(1024, [(bytes(ip), _rand_macs(rng, 1)[0].tobytes())
+                           for ip in dst6[rng.permutation(n_hosts)[:600]]])
+    specs, rules = _flow_rules(rng, n_rules, dst4, dst6, ports, max_cover)
+
+    # per-rule arrays, and a last pseudo-rule with every field a wildcard (the strays)
+    R = len(specs) + 1
+    fam = np.array([s["fam"] for s in specs] + [4])
+    agn = np.array([s["ver"] == 0 and s["ls"] is None and s["ld"] is None for s in specs] + [True])
+    src4 = np.array([s["src"] if s["fam"] == 4 else V4_SRC_BASE for s in specs] + [V4_SRC_BASE],
+                    dtype=np.uint64)
+    m4s = np.array([ipv4_mask(s["ls"]) if s["fam"] == 4 and s["ls"] is not None else
+                    ipv4_mask(8) for s in specs] + [ipv4_mask(8)], dtype=np.uint64)
+    src6 = np.stack([np.frombuffer(s["src"], np.uint8) if s["fam"] == 6 else
+                     np.frombuffer(V6_SRC_PRE + bytes(12), np.uint8) for s in specs] +
+                    [np.frombuffer(V6_SRC_PRE + bytes(12), np.uint8)])
+    m6s = np.stack([_v6_mask_arr(s["ls"] if s["fam"] == 6 and s["ls"] is not None else 32)
+                    for s in specs] + [_v6_mask_arr(32)])
+    pools = [s["pool"] if s["pool"] is not None else None for s in specs] + [None]
+    cnt = np.array([len(p) if p is not None else 0 for p in pools])
+    off = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    flat = np.concatenate([p for p in pools if p is not None] + [np.zeros(1, np.int64)])
+    r_proto = np.array([s["proto"] for s in specs] + [0])
+    r_sport = np.array([s["sport"] for s in specs] + [0])
+    r_dport = np.array([s["dport"] for s in specs] + [0])
+
+    j = rng.integers(0, R - 1, size=n)
+    j = np.where(rng.random(n) < stray, R - 1, j)
+    # family: the rule's, or 70/30 for rules that constrain no address (and strays)
+    is6 = np.where(agn[j], rng.random(n) < 0.3, fam[j] == 6)
+    r4 = np.nonzero(~is6)[0]
+    r6 = np.nonzero(is6)[0]
+    # protocol, ports
+    p4 = rng.choice(C_PROTO4[0], size=n, p=C_PROTO4[1])
+    p6 = rng.choice(C_PROTO6[0], size=n, p=C_PROTO6[1])
+    proto = np.where(r_proto[j] != 0, r_proto[j], np.where(is6, p6, p4))
+    proto = np.where(is6 & (proto == 1), 17, proto)   # (an ICMP rule of a version-0 draw)
+    sport = np.where(r_sport[j] != 0, r_sport[j], ports[rng.integers(0, len(ports), size=n)])
+    dport = np.where(r_dport[j] != 0, r_dport[j], ports[rng.integers(0, len(ports), size=n)])
+    sport = sport.astype(np.uint32)
+    dport = dport.astype(np.uint32)
+    # destinations: a pool host inside the rule's prefix, or any pool host
+    inside = flat[off[j] + (rng.random(n) * np.maximum(cnt[j], 1)).astype(np.int64)]
+    pick = np.where(cnt[j] > 0, inside, rng.integers(0, n_hosts, size=n))
+    # sources: random bits below the rule's prefix
+    s4 = (src4[j] & m4s[j]) | (rng.integers(0, 1 << 32, size=n, dtype=np.uint64) & ~m4s[j]
+                               & np.uint64(0xFFFFFFFF))
+    s6 = (src6[j] & m6s[j]) | (rng.integers(0, 256, size=(n, 16), dtype=np.uint8) & ~m6s[j])
+
+    imix = rng.choice(np.array([64, 570, 1518]), size=n, p=[7 / 12, 4 / 12, 1 / 12])
+    hdr_len = np.where(is6, 54, 34) + np.where(proto == 6, 20, 8)
+    size = np.maximum(imix, hdr_len)
+    h = np.zeros((n, 128), dtype=np.uint8)
+    _macs(h, rng)
+    ttl = rng.integers(1, 129, size=n)
+    build_ipv4(h, r4, src=s4[r4], dst=dst4[pick[r4]], proto=proto[r4], ttl=ttl[r4],
+               ihl=np.full(len(r4), 5), total_len=size[r4] - 14,
+               l4_ports=(sport[r4], dport[r4]), tcp_doff=np.full(len(r4), 5),
+               icmp=(dport[r4] >> 8, dport[r4] & 0xFF, sport[r4]), rng=rng)
+    build_ipv6(h, r6, src16=s6[r6], dst16=dst6[pick[r6]], nh=proto[r6], hop=ttl[r6],
+               payload_len=size[r6] - 54, sport=sport[r6], dport=dport[r6],
+               tcp_doff=np.full(len(r6), 5))
+    frames, desc = pack_frames(h, size)
+    return Workload("C", frames, desc, rules, n_rules, arp, ndp)
+
+
+# ---------------------------------------------------------------------------------------------
 # config D — 64k rules, variable-length headers, malformed traffic, v4/v6 interleaved
 # ---------------------------------------------------------------------------------------------
 
