@@ -2545,6 +2545,7 @@ struct upe_gpu_ctx {
     uint32_t host_slots = 4;       // device slots of the host round trip (UPE_GPU_HOST_SLOTS, 2..8)
     // the kernel without look-back (kNoLB): the launches' start-state agreement, written by the
     // device into host-mapped memory, and the first launch whose report counts
+    hipEvent_t marks[4] = {};      // worker loop completion marks (upe_gpu_mark)
     unsigned long long* agree_h = nullptr;
     unsigned long long* agree_d = nullptr;
     uint64_t lb_reset_k = 0;
@@ -3004,6 +3005,8 @@ void upe_gpu_close(upe_gpu_ctx_t* c) {
     if (c->ring_wg) (void)hipFree(c->ring_wg);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+    for (hipEvent_t e : c->marks)
+        if (e) (void)hipEventDestroy(e);
     for (auto& sl : c->hs) {
         for (void* b : {(void*)sl.frames, (void*)sl.desc, (void*)sl.verdict, (void*)sl.hdr})
             if (b) (void)hipFree(b);
@@ -4835,6 +4838,23 @@ int upe_gpu_process_segmented(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_
         return -1;
     HIP_TRY(hipStreamSynchronize(s));
     if (n_writes) *n_writes = writes;
+    return 0;
+}
+
+// For the worker loop (upe_worker.c), not part of the ABI: a completion mark after everything
+// queued so far on the context's stream, and a wait for it, so that the loop walks batch k - 1
+// while batch k is on the GPU.
+__attribute__((visibility("hidden"))) int upe_gpu_mark(upe_gpu_ctx_t* c, int slot) {
+    if (!c || slot < 0 || slot >= 4) return fail("bad mark");
+    DEV_SCOPE(c->device);
+    if (!c->marks[slot]) HIP_TRY(hipEventCreateWithFlags(&c->marks[slot], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->marks[slot], c->stream));
+    return 0;
+}
+__attribute__((visibility("hidden"))) int upe_gpu_mark_wait(upe_gpu_ctx_t* c, int slot) {
+    if (!c || slot < 0 || slot >= 4 || !c->marks[slot]) return fail("bad mark");
+    DEV_SCOPE(c->device);
+    HIP_TRY(hipEventSynchronize(c->marks[slot]));
     return 0;
 }
 

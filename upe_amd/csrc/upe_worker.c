@@ -20,10 +20,20 @@
  *    (src/worker.c:280), parsed / matched / dropped per packet (src/worker.c:119-153), the TX
  *    accounting above.
  *
+ * Two batches are in flight (round 5): batch k is launched and, while the GPU classifies it, the
+ * loop walks batch k - 1's verdicts (the TX calls, the frees) and then gathers batch k + 1 into
+ * the slot k - 1 used — the GPU's share of a batch hides behind the host's.  A batch cut at a
+ * table-writing packet drains the pipeline instead (walk k - 1, wait for k, walk it, apply the
+ * write, upload the tables) before anything later is launched, and so does an empty ring and a
+ * change polled between bursts: the order of every call is the sequential loop's.  The walk
+ * reads nothing of a frame it does not rewrite: the handle's data pointer and length are kept
+ * from the gather.
+ *
  * Two ways to get a batch to the GPU (cfg->pool_base): copy each frame's header window into
- * pinned staging and run the DMA round trip in emit mode (the 16-byte records are then applied to
- * the caller's buffers, upe_hdr_apply), or leave the frames where they are in a registered pool and
- * let the kernel classify and rewrite them there (upe_gpu_process_mapped).
+ * pinned staging, ship it with the descriptors, classify in emit mode and bring back the verdicts
+ * and 16-byte records (applied to the caller's buffers in the walk, upe_hdr_apply) — or leave the
+ * frames where they are in a registered pool and let the kernel classify and rewrite them there
+ * (upe_gpu_process_mapped, nothing copied).
  */
 #define _GNU_SOURCE
 #include <stdlib.h>
@@ -32,10 +42,31 @@
 
 #include "../../include/upe_gpu.h"
 
-/* upe_gpu.hip: sets the calling thread's upe_gpu_last_error() message (not part of the ABI) */
+/* upe_gpu.hip, not part of the ABI: the calling thread's upe_gpu_last_error() message, and
+ * completion marks on the context's stream */
 int upe_gpu_set_last_error(const char *msg);
+int upe_gpu_mark(upe_gpu_ctx_t *ctx, int slot);
+int upe_gpu_mark_wait(upe_gpu_ctx_t *ctx, int slot);
 
 #define WIN UPE_HDR_WINDOW
+#define NSLOT 2
+
+/* One batch: gathered, then launched (busy), then walked. */
+typedef struct {
+    void **bufs;           /* handles in arrival order */
+    uint8_t **data;        /* their frames, as data() gave them at the gather */
+    size_t n;
+    int cut;               /* ends with a table-writing control packet */
+    int busy;              /* launched, not walked yet */
+    uint64_t *desc;        /* pinned: offset << 16 | len */
+    uint32_t *verdict;     /* pinned (mapped mode: written by the kernel over the link) */
+    uint8_t *win;          /* window mode: pinned header windows */
+    upe_hdr_rec_t *rec;    /* window mode: pinned records */
+    uint8_t *d_win;        /* window mode: device copies */
+    uint64_t *d_desc;
+    uint32_t *d_verdict;
+    upe_hdr_rec_t *d_rec;
+} slot_t;
 
 typedef struct {
     upe_gpu_ctx_t *ctx;
@@ -45,13 +76,9 @@ typedef struct {
     unsigned burst;
     uint8_t *pool;     /* mapped mode: registered region the frames lie in */
     size_t pool_bytes;
-    /* the batch being gathered: handles in arrival order, and the pinned arrays the GPU reads */
-    void **bufs;
-    size_t n;
-    uint64_t *desc;
-    uint32_t *verdict;
-    uint8_t *win;          /* window mode: cap header windows + UPE_FRAME_TAIL */
-    upe_hdr_rec_t *rec;    /* window mode: records */
+    slot_t s[NSLOT];
+    int g;             /* the slot being gathered */
+    int o;             /* the busy slot launched before it, or -1 */
     /* sizes of the bursts popped and not yet flushed, oldest first (a ring) */
     unsigned *bq;
     size_t bq_cap, bq_head, bq_len;
@@ -115,33 +142,57 @@ static void flush_tx(loop_t *L) {
     }
 }
 
-/* Classify the gathered batch on the GPU, then walk it in packet order doing what
- * process_packet's exits and worker_main's flush do.  cut: the batch ends with a table-writing
- * control packet, whose write is applied and uploaded before anything else is classified. */
-static int run_batch(loop_t *L, int cut) {
-    const size_t n = L->n;
-    if (n == 0) return 0;
+/* Queue slot k's batch on the GPU (asynchronously) and mark its completion. */
+static int launch(loop_t *L, int k) {
+    slot_t *S = &L->s[k];
+    const size_t n = S->n;
     int rc;
     if (L->pool) {
-        rc = upe_gpu_process_mapped(L->ctx, L->pool, L->desc, L->verdict, n, NULL);
-        if (rc == 0) rc = upe_gpu_sync(L->ctx, NULL);
+        rc = upe_gpu_process_mapped(L->ctx, L->pool, S->desc, S->verdict, n, NULL);
     } else {
-        rc = upe_gpu_process_host_emit(L->ctx, L->win, n * WIN + UPE_FRAME_TAIL, L->desc,
-                                       L->verdict, L->rec, n, 0, -1);
+        rc = upe_gpu_memcpy_h2d(L->ctx, S->d_win, S->win, n * WIN, NULL);
+        if (rc == 0) rc = upe_gpu_memcpy_h2d(L->ctx, S->d_desc, S->desc, n * sizeof(uint64_t), NULL);
+        if (rc == 0)
+            rc = upe_gpu_process_emit(L->ctx, S->d_win, S->d_desc, S->d_verdict, S->d_rec, n, NULL);
+        if (rc == 0)
+            rc = upe_gpu_memcpy_d2h(L->ctx, S->verdict, S->d_verdict, n * sizeof(uint32_t), NULL);
+        if (rc == 0)
+            rc = upe_gpu_memcpy_d2h(L->ctx, S->rec, S->d_rec, n * sizeof(upe_hdr_rec_t), NULL);
     }
-    if (rc != 0) return -1;
+    if (rc == 0) rc = upe_gpu_mark(L->ctx, k);
+    S->busy = rc == 0;
+    return rc;
+}
+
+/* Wait for slot k's batch, then walk it in packet order doing what process_packet's exits and
+ * worker_main's flush do.  A cut batch's last packet writes the tables, which are re-uploaded
+ * before anything else is launched. */
+static int walk(loop_t *L, int k) {
+    slot_t *S = &L->s[k];
+    if (upe_gpu_mark_wait(L->ctx, k) != 0) return -1;
+    const size_t n = S->n;
     for (size_t i = 0; i < n; i++) {
-        void *b = L->bufs[i];
-        uint8_t *d = L->ops->data(L->user, b);
-        const size_t len = L->ops->len(L->user, b);
-        const uint32_t v = L->verdict[i];
+        void *b = S->bufs[i];
+        uint8_t *d = S->data[i];
+        const size_t len = (size_t)(S->desc[i] & 0xFFFFu);
+        const uint32_t v = S->verdict[i];
         const uint32_t code = UPE_VERDICT_CODE(v);
         if (!L->pool) {
-            /* window mode: the rewritten bytes into the caller's buffer */
-            if (code == UPE_V_FWD)
-                upe_hdr_apply(d, &L->rec[i]);
-            else if (v & UPE_VF_ARP_REPLY)
-                memcpy(d, L->win + i * WIN, len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT);
+            /* window mode: the rewritten bytes into the caller's buffer (an answered ARP
+             * request ends a cut batch, so nothing is queued behind it: a synchronous copy) */
+            if (code == UPE_V_FWD) {
+                upe_hdr_apply(d, &S->rec[i]);
+            } else if (v & UPE_VF_ARP_REPLY) {
+                const size_t c = len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT;
+                if (upe_gpu_memcpy_d2h(L->ctx, d, S->d_win + i * WIN, c, NULL) != 0 ||
+                    upe_gpu_sync(L->ctx, NULL) != 0) {
+                    /* the packets not walked yet stay held (for the drain) */
+                    memmove(S->bufs, S->bufs + i, (n - i) * sizeof(void *));
+                    S->n = n - i;
+                    S->busy = 0;
+                    return -1;
+                }
+            }
         }
         if (L->left == 0) { /* the next burst starts here */
             L->left = L->bq[L->bq_head];
@@ -149,7 +200,7 @@ static int run_batch(loop_t *L, int cut) {
             L->bq_len--;
         }
         if (v & UPE_VF_ARP_LEARN) L->c.arp_learn++;
-        if (cut && i + 1 == n) control_writes(L, d, len, v); /* arp_update before the reply */
+        if (S->cut && i + 1 == n) control_writes(L, d, len, v); /* arp_update before the reply */
         if (v & UPE_VF_ARP_REPLY) {
             L->c.arp_reply++;
             (void)L->ops->tx_send(L->user, d, len); /* src/worker.c:52 */
@@ -171,18 +222,90 @@ static int run_batch(loop_t *L, int cut) {
         }
         if (--L->left == 0) flush_tx(L); /* the burst is complete */
     }
-    L->n = 0;
+    const int cut = S->cut;
+    S->n = 0;
+    S->cut = 0;
+    S->busy = 0;
     if (cut && L->ops->load_neigh(L->user, L->ctx) != 0) return -1;
     if (L->ops->publish) L->ops->publish(L->user, L->ctx, &L->c);
     return 0;
 }
 
+/* Every batch held to completion, oldest first: the gathering slot's is launched first if it
+ * holds packets.  Afterwards nothing is on the GPU. */
+static int finish_all(loop_t *L) {
+    slot_t *G = &L->s[L->g];
+    if (G->n > 0 && !G->busy && launch(L, L->g) != 0) return -1;
+    if (L->o >= 0 && walk(L, L->o) != 0) return -1;
+    L->o = -1;
+    if (G->busy && walk(L, L->g) != 0) return -1;
+    return 0;
+}
+
+/* The gathering slot is complete (full, or cut): launch it; walk the older batch meanwhile and
+ * gather the next one into its slot — or, after a cut, drain everything. */
+static int advance(loop_t *L) {
+    if (L->s[L->g].cut) return finish_all(L);
+    if (launch(L, L->g) != 0) return -1;
+    if (L->o >= 0 && walk(L, L->o) != 0) return -1;
+    L->o = L->g;
+    L->g = (L->g + 1) % NSLOT;
+    return 0;
+}
+
 /* Drop everything the loop holds after an error (the reference would have freed it). */
 static void drain(loop_t *L) {
-    for (size_t i = 0; i < L->n; i++) L->ops->free_buf(L->user, L->bufs[i]);
-    L->n = 0;
+    if (L->o >= 0) (void)upe_gpu_mark_wait(L->ctx, L->o);   /* the GPU is done with them */
+    if (L->s[L->g].busy) (void)upe_gpu_mark_wait(L->ctx, L->g);
+    for (int k = 0; k < NSLOT; k++) {
+        for (size_t i = 0; i < L->s[k].n; i++) L->ops->free_buf(L->user, L->s[k].bufs[i]);
+        L->s[k].n = 0;
+    }
     for (int i = 0; i < L->tx_count; i++) L->ops->free_buf(L->user, L->tx_bufs[i]);
     L->tx_count = 0;
+}
+
+static void free_slots(loop_t *L) {
+    for (int k = 0; k < NSLOT; k++) {
+        slot_t *S = &L->s[k];
+        free(S->bufs);
+        free(S->data);
+        if (S->desc) upe_gpu_host_free(S->desc);
+        if (S->verdict) upe_gpu_host_free(S->verdict);
+        if (S->win) upe_gpu_host_free(S->win);
+        if (S->rec) upe_gpu_host_free(S->rec);
+        if (S->d_win) upe_gpu_free(L->ctx, S->d_win);
+        if (S->d_desc) upe_gpu_free(L->ctx, S->d_desc);
+        if (S->d_verdict) upe_gpu_free(L->ctx, S->d_verdict);
+        if (S->d_rec) upe_gpu_free(L->ctx, S->d_rec);
+    }
+}
+
+static int alloc_slots(loop_t *L) {
+    for (int k = 0; k < NSLOT; k++) {
+        slot_t *S = &L->s[k];
+        S->bufs = malloc((L->cap + L->burst) * sizeof(void *));
+        S->data = malloc((L->cap + L->burst) * sizeof(uint8_t *));
+        S->desc = upe_gpu_host_alloc(L->cap * sizeof(uint64_t));
+        S->verdict = upe_gpu_host_alloc(L->cap * sizeof(uint32_t));
+        if (!S->bufs || !S->data || !S->desc || !S->verdict) return -1;
+        if (!L->pool) {
+            S->win = upe_gpu_host_alloc(L->cap * WIN + UPE_FRAME_TAIL);
+            S->rec = upe_gpu_host_alloc(L->cap * sizeof(upe_hdr_rec_t));
+            S->d_win = upe_gpu_malloc(L->ctx, L->cap * WIN + UPE_FRAME_TAIL);
+            S->d_desc = upe_gpu_malloc(L->ctx, L->cap * sizeof(uint64_t));
+            S->d_verdict = upe_gpu_malloc(L->ctx, L->cap * sizeof(uint32_t));
+            S->d_rec = upe_gpu_malloc(L->ctx, L->cap * sizeof(upe_hdr_rec_t));
+            if (!S->win || !S->rec || !S->d_win || !S->d_desc || !S->d_verdict || !S->d_rec)
+                return -1;
+            memset(S->win, 0, L->cap * WIN + UPE_FRAME_TAIL);
+            /* the tail past the last window (read as zero by the kernel's window loads) */
+            if (upe_gpu_memcpy_h2d(L->ctx, S->d_win + L->cap * WIN, S->win, UPE_FRAME_TAIL, NULL) ||
+                upe_gpu_sync(L->ctx, NULL))
+                return -1;
+        }
+    }
+    return 0;
 }
 
 int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *user,
@@ -201,51 +324,48 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
     L.burst = cfg && cfg->burst ? cfg->burst : 32;
     L.pool = cfg ? cfg->pool_base : NULL;
     L.pool_bytes = cfg ? cfg->pool_bytes : 0;
-    const long idle = cfg && cfg->idle_ns ? (long)cfg->idle_ns : 1000;
+    L.o = -1;
+    const unsigned idle = cfg && cfg->idle_ns ? cfg->idle_ns : 1000;
+    const struct timespec nap = {(time_t)(idle / 1000000000u), (long)(idle % 1000000000u)};
     if (L.burst > UPE_TX_BATCH_MAX) return upe_gpu_set_last_error("burst exceeds UPE_TX_BATCH_MAX");
     if (L.cap > ((size_t)1 << 24)) return upe_gpu_set_last_error("batch exceeds 2^24 packets");
     if (L.pool && ((uintptr_t)L.pool & 15u))
         return upe_gpu_set_last_error("pool_base must be 16-byte aligned");
     if (L.pool && L.pool_bytes < UPE_FRAME_TAIL)
         return upe_gpu_set_last_error("pool_bytes must give the registered region's size");
-    L.bufs = malloc((L.cap + L.burst) * sizeof(void *));
-    L.bq_cap = L.cap + 2;
+    /* every burst popped and not yet flushed: those of two batches in flight and a partial one */
+    L.bq_cap = NSLOT * (L.cap + L.burst) + 4;
     L.bq = malloc(L.bq_cap * sizeof(unsigned));
-    L.desc = upe_gpu_host_alloc(L.cap * sizeof(uint64_t));
-    L.verdict = upe_gpu_host_alloc(L.cap * sizeof(uint32_t));
-    if (!L.pool) {
-        L.win = upe_gpu_host_alloc(L.cap * WIN + UPE_FRAME_TAIL);
-        L.rec = upe_gpu_host_alloc(L.cap * sizeof(upe_hdr_rec_t));
-    }
     int rc = 0;
-    if (!L.bufs || !L.bq || !L.desc || !L.verdict || (!L.pool && (!L.win || !L.rec))) {
+    if (!L.bq || alloc_slots(&L) != 0) {
         rc = upe_gpu_set_last_error("out of memory (worker loop buffers)");
         goto out;
     }
     void *burst[UPE_TX_BATCH_MAX];
     for (;;) {
         const unsigned k = ops->pop_burst(user, burst, L.burst); /* src/worker.c:268 */
+        slot_t *G = &L.s[L.g];
         /* a change between bursts (polled after the pop: a burst pushed after the change was
          * made is classified with it): the packets held finish with the old state first */
-        if (ops->poll && ops->poll(user) &&
-            (run_batch(&L, 0) != 0 || ops->sync(user, ctx) != 0)) {
-            for (unsigned r = 0; r < k; r++) L.bufs[L.n++] = burst[r];
+        if (ops->poll && ops->poll(user) && (finish_all(&L) != 0 || ops->sync(user, ctx) != 0)) {
+            G = &L.s[L.g];
+            for (unsigned r = 0; r < k; r++) G->bufs[G->n++] = burst[r];
             goto fail;
         }
         if (k == 0) {
-            if (L.n > 0) { /* the ring is empty: classify what is held now */
-                if (run_batch(&L, 0) != 0) goto fail;
+            if (G->n > 0 || L.o >= 0) { /* the ring is empty: classify what is held now */
+                if (finish_all(&L) != 0) goto fail;
                 continue;
             }
             if (ops->stop(user)) break; /* stop signal + ring empty, src/worker.c:270-273 */
-            struct timespec ts = {0, idle};
-            nanosleep(&ts, NULL);
+            nanosleep(&nap, NULL);
             continue;
         }
         L.c.pkts_in += k; /* src/worker.c:280 */
         L.bq[(L.bq_head + L.bq_len) % L.bq_cap] = k;
         L.bq_len++;
         for (unsigned j = 0; j < k; j++) {
+            G = &L.s[L.g];
             void *b = burst[j];
             uint8_t *d = ops->data(user, b);
             const size_t len = ops->len(user, b);
@@ -256,20 +376,22 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
                     len > 0xFFFFu) {
                     upe_gpu_set_last_error(
                         "a frame is not 16-byte aligned inside the registered pool");
-                    for (unsigned r = j; r < k; r++) L.bufs[L.n++] = burst[r];
+                    for (unsigned r = j; r < k; r++) G->bufs[G->n++] = burst[r];
                     goto fail;
                 }
-                L.desc[L.n] = UPE_DESC(off, len);
+                G->desc[G->n] = UPE_DESC(off, len);
             } else {
-                const size_t c = len < WIN ? len : WIN;
-                memcpy(L.win + L.n * WIN, d, c);
-                L.desc[L.n] = UPE_DESC(L.n * WIN, len);
+                /* (bytes of the window past len are never read: stale ones may stay) */
+                memcpy(G->win + G->n * WIN, d, len < WIN ? len : WIN);
+                G->desc[G->n] = UPE_DESC(G->n * WIN, len);
             }
-            L.bufs[L.n++] = b;
-            const int cut = is_table_write(d, len);
-            if ((cut || L.n == L.cap) && run_batch(&L, cut) != 0) {
+            G->data[G->n] = d;
+            G->bufs[G->n++] = b;
+            G->cut = is_table_write(d, len);
+            if ((G->cut || G->n == L.cap) && advance(&L) != 0) {
                 /* the rest of this burst is held by nobody else: keep it for the drain */
-                for (unsigned r = j + 1; r < k; r++) L.bufs[L.n++] = burst[r];
+                G = &L.s[L.g];
+                for (unsigned r = j + 1; r < k; r++) G->bufs[G->n++] = burst[r];
                 goto fail;
             }
         }
@@ -280,11 +402,7 @@ fail:
     drain(&L);
 out:
     if (counters) *counters = L.c;
-    free(L.bufs);
     free(L.bq);
-    if (L.desc) upe_gpu_host_free(L.desc);
-    if (L.verdict) upe_gpu_host_free(L.verdict);
-    if (L.win) upe_gpu_host_free(L.win);
-    if (L.rec) upe_gpu_host_free(L.rec);
+    free_slots(&L);
     return rc;
 }
