@@ -54,7 +54,13 @@ WORKLOADS = {
     "A": "A: 10k x 64B UDP/IPv4 pcap-replay records, rules.example (configs[0], the reference's "
          "own CPU case), replayed as device-resident batches",
     "B": "B: 1M x 64B UDP/IPv4, 8 rules, ARP 240/256 hit (BASELINE configs[1])",
-    "C": "C: 1M IMIX 64/570/1518 v4+v6, 1k 5-tuple rules, ARP+NDP L3 fwd (configs[2])",
+    "C": "C: 1M IMIX 64/570/1518 v4+v6, 1k 5-tuple rules cut from the traffic's flows (first "
+         "matches spread over the whole table, both families), ARP+NDP L3 fwd (configs[2], "
+         "synth.config_c_flows)",
+    "C3": "C (seed-3 draw, rounds 1-4): 1M IMIX v4+v6, 1k random 5-tuple rules; every IPv4 packet "
+          "stops by sorted rule 11, every IPv6 packet at rule 0 (synth.config_c)",
+    "C6": "C seed-3 with its family-wide wildcard rules last: IPv6 forwarded through NDP, IPv6 "
+          "first matches spread (synth.config_c(v6_forwarding=True))",
     "D": "D: 16M mixed/malformed, 64k rules (configs[3])",
 }
 
@@ -157,6 +163,10 @@ def hbm_probe(torch, dev, gib: int = 4, reps: int = 10) -> dict:
     return {"copy_GBps": round(2 * n * reps / t_copy / 1e9, 1),
             "read_GBps": round(n * reps / t_read / 1e9, 1),
             "method": f"torch copy_ (read + write) and sum (read) over {gib} GiB, HIP events"}
+
+
+def rule_index_name(kind: int) -> str:
+    return {0: "linear scan", 1: "tuple-space index", 2: "decision tree"}.get(kind, str(kind))
 
 
 def pmc_traffic(config: str, packets: int, mode: str):
@@ -380,17 +390,20 @@ def host_mapped(worker, wl, reps: int, emit: bool) -> dict:
 
 
 def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, mode: str,
-             copies_cap: int, v6_forwarding: bool = False) -> dict:
-    """The IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
+             copies_cap: int, kind: str = "C") -> dict:
+    """An IMIX workload (config C: 64/570/1518 B, IPv4 + IPv6, 1k rules, ARP + NDP forwarding)
     timed the same way as `value`, on every rank at once after the main region, so that a
     multi-GPU run reports the 64 B and the IMIX rates at each N (BASELINE north_star).  Each rank
     takes its own shard (seed 3 + 1000 * rank); `copies_cap` distinct copies of the batch
-    (32 x 373 MB, past the Infinity Cache) are cycled.  Not `value`.  v6_forwarding: the same
-    traffic with the rule table's family-wide wildcards last, so that IPv6 is forwarded through
-    the NDP lookup (config C's seed-3 draw drops all IPv6 at rule 0), reported as `imix_v6fwd`."""
+    (32 x ~370 MB, past the Infinity Cache) are cycled.  Not `value`.  kind: "C" the flow-derived
+    rules (first matches spread over the table: the `imix` leg from round 5), "C3" the seed-3 draw
+    of rounds 1-4 (`imix_seed3`: IPv4 stops by rule 11, IPv6 at rule 0), "C6" the seed-3 draw
+    with its family-wide wildcards last (`imix_v6fwd`: IPv6 forwarded through NDP)."""
     from upe_amd import gpu, shard, synth
 
-    wl = synth.config_c(seed=3 + 1000 * rank, v6_forwarding=v6_forwarding)
+    seed = 3 + 1000 * rank
+    wl = (synth.config_c_flows(seed=seed) if kind == "C" else
+          synth.config_c(seed=seed, v6_forwarding=kind == "C6"))
     n = wl.n
     worker = gpu.GpuWorker(local, wl.capacity)
     worker.configure(wl)
@@ -433,22 +446,78 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     v = verdict.cpu().numpy().view(np.uint32).copy()
     cms, gms, launches = worker.timing_read()
     cms += gms
+    idx_kind = worker.rule_index_kind()
     worker.close()
     del pool, desc, verdict, hdr
     bpp = algorithmic_bytes(wl, v, emit=mode == "emit")
     kern_s = cms / launches / 1e3 if launches else float("nan")
     achieved = float(bpp.sum()) / kern_s / 1e9
-    return {"workload": WORKLOADS["C"], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
+    return {"workload": WORKLOADS[kind], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
             "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps,
             "packets_per_gpu_step": n,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "kernel_ms": round(kern_s * 1e3, 5),
                          "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
-                         "traffic": pmc_traffic("C", n, mode)},
+                         "traffic": pmc_traffic({"C": "CF", "C3": "C", "C6": "C6"}[kind], n,
+                                                mode),
+                         "rule_index": rule_index_name(idx_kind)},
             "format": "packed frames (upe_gpu_process_emit)",
             "what": f"all ranks at once after the main region, {copies} distinct batch copies "
                     "cycled, same timing protocol as value (barrier, max over ranks)"}
+
+
+def strong_leg(torch, dev, dist, rank: int, world: int, local: int, kind: str, steps: int,
+               warmup: int) -> dict:
+    """Strong scaling: ONE batch — config B's 1M 64 B packets, or config
+    C's 1M IMIX packets (flow-derived rules) — split into `world` contiguous static shards
+    (shard.shard_workload: rank r takes [r n / world, (r + 1) n / world), tables replicated, its
+    own calloc'd L1 state, no collective on the data path).  Every rank classifies its shard
+    `steps` times (emit mode, 8 distinct copies cycled); value = the batch's packets x steps / the
+    slowest rank's time.  The driver's runs at N = 1, 2, 4, 8 give the strong-scaling curve beside
+    the weak-scaling `value` (each rank its own full batch)."""
+    from upe_amd import gpu, shard, synth
+
+    whole = synth.config_b() if kind == "B" else synth.config_c_flows()
+    total_n = whole.n
+    wl = shard.shard_workload(whole, rank, world)
+    del whole
+    n = wl.n
+    worker = gpu.GpuWorker(local, wl.capacity)
+    worker.configure(wl)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    fbytes = int(wl.frames.nbytes)
+    stride = (fbytes + 255) // 256 * 256
+    copies = 8
+    pristine = torch.from_numpy(wl.frames).to(dev)
+    pool = torch.empty(copies * stride, dtype=torch.uint8, device=dev)
+    for c in range(copies):
+        pool[c * stride: c * stride + fbytes].copy_(pristine)
+    del pristine
+    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    verdict = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    hdr = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=dev)
+    base = pool.data_ptr()
+    ptrs = [base + (k % copies) * stride for k in range(warmup + steps)]
+    worker.process_batches_emit(ptrs[:warmup], desc, verdict, hdr, n, sh)
+    torch.cuda.synchronize(dev)
+    timed = gpu.GpuWorker.frames_list(ptrs[warmup:])
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    worker.process_batches_emit(timed, desc, verdict, hdr, n, sh)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    worker.close()
+    del pool, desc, verdict, hdr
+    return {"workload": WORKLOADS[kind] + f", one batch split over {world} GPU(s)",
+            "value": round(total_n * steps / elapsed / 1e6, 2), "unit": "Mpps",
+            "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps,
+            "packets_per_step": total_n, "packets_this_rank": n, "scaling": "strong",
+            "what": "all ranks at once after the main region, barrier + max over ranks"}
 
 
 VALU_PEAK_G = 1024 * 2.4 / 2   # G wave64 VALU instructions/s: 1024 SIMD-32s, one per 2 cycles
@@ -660,8 +729,13 @@ def main() -> None:
                     help="skip the IMIX leg (config C timed after the main region on every rank, "
                          "reported as \"imix\" beside value; config B runs only)")
     ap.add_argument("--imix-v6fwd", type=int, default=1,
-                    help="1: also time config C with its family-wide wildcards last (IPv6 "
-                         "forwarded through NDP, deep rule scans), reported as \"imix_v6fwd\"")
+                    help="1: also time the seed-3 config C draw of rounds 1-4 (\"imix_seed3\") "
+                         "and the same with its family-wide wildcards last (IPv6 forwarded "
+                         "through NDP, \"imix_v6fwd\")")
+    ap.add_argument("--strong", type=int, default=1,
+                    help="1: also time strong scaling (SURVEY.md §8(d) row E): one config B batch "
+                         "and one config C batch split into WORLD contiguous shards, reported as "
+                         "\"strong\" beside the weak-scaling value")
     ap.add_argument("--imix-copies", type=int, default=32)
     ap.add_argument("--config-d-steps", type=int, default=20,
                     help="timed steps of the config D leg (16M packets, 64k rules; N=1 config B "
@@ -705,7 +779,7 @@ def main() -> None:
         print(f"bench: no NUMA pinning ({e})", file=sys.stderr)
 
     # this rank's static shard: a full batch of the configuration, its own seed
-    make = {"A": synth.config_a, "B": synth.config_b, "C": synth.config_c,
+    make = {"A": synth.config_a, "B": synth.config_b, "C": synth.config_c_flows,
             "D": synth.config_d}[args.config]
     kw = {"seed": {"A": 1, "B": 2, "C": 3, "D": 4}[args.config] + 1000 * rank}
     if args.packets:
@@ -809,13 +883,19 @@ def main() -> None:
     if args.workers_per_gpu > 1:
         shared = shared_gpu_workers(torch, dev, wl, worker, pool, stride, copies, desc,
                                     args.workers_per_gpu, args.steps)
-    imix = imix6 = None
+    imix = imix3 = imix6 = None
     if args.config == "B" and not args.no_imix and not args.packets:
         imix = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
                         args.imix_copies)
         if args.imix_v6fwd:
+            imix3 = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
+                             args.imix_copies, kind="C3")
             imix6 = imix_leg(torch, dev, dist, rank, local, args.steps, args.warmup, args.mode,
-                             args.imix_copies, v6_forwarding=True)
+                             args.imix_copies, kind="C6")
+    strong = None
+    if args.config == "B" and args.strong and not args.packets:
+        strong = {k: strong_leg(torch, dev, dist, rank, world, local, k, args.steps, args.warmup)
+                  for k in ("B", "C")}
     ring = None
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
@@ -862,7 +942,7 @@ def main() -> None:
 
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first, emit=args.mode == "emit")
-        traffic = pmc_traffic(args.config, n, args.mode)
+        traffic = pmc_traffic({"C": "CF"}.get(args.config, args.config), n, args.mode)
         bytes_per_launch = float(bpp.sum())
         # a step's kernels: the classify launch plus (tables over 4096 rules) the rule_stats
         # group-by; finalize_ms is the group-by's share (0 for smaller tables)
@@ -898,7 +978,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "traffic_source": (f"profiles/pmc_config{args.config}"
+                "traffic_source": (f"profiles/pmc_config{ {'C': 'CF'}.get(args.config, args.config)}"
                                    f"{'_emit' if args.mode == 'emit' else ''}.json (rocprofv3 "
                                    "PMC, 2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
                 "kernel": "upe_classify",
@@ -925,9 +1005,12 @@ def main() -> None:
             out["other_mode"] = other
         if imix:
             out["imix"] = imix
+        if imix3:
+            out["imix_seed3"] = imix3
         if imix6:
-            imix6["workload"] = WORKLOADS["C"] + ", family-wide wildcard rules last (IPv6 forwarded)"
             out["imix_v6fwd"] = imix6
+        if strong:
+            out["strong"] = strong
         if ring:
             out["ring"] = ring
         if dleg:
