@@ -27,7 +27,8 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {"B": lambda: synth.config_b(n=300_000, seed=41),
-         "C": lambda: synth.config_c(n=200_000, seed=42)}
+         "C": lambda: synth.config_c(n=200_000, seed=42),
+         "CF": lambda: synth.config_c_flows(n=200_000, seed=43)}
 
 
 def _free_port() -> int:
@@ -74,7 +75,7 @@ def _rank(rank, world, port, case, emit, q):
 
 
 @pytest.mark.parametrize("emit", [False, True])
-@pytest.mark.parametrize("case", ["B", "C"])
+@pytest.mark.parametrize("case", ["B", "C", "CF"])
 def test_two_rank_static_shards_on_gpu(case, emit):
     world = 2
     ctx = mp.get_context("spawn")
@@ -99,13 +100,14 @@ def test_two_rank_static_shards_on_gpu(case, emit):
 def test_bench_two_ranks():
     """bench.py's N > 1 path end to end: torch.distributed.run with two ranks on the one GPU
     (gloo for the barrier and the max / sum over ranks, as UPE_BENCH_DIST_BACKEND allows on a
-    one-GPU box), config B plus the IMIX leg, each rank its own shard."""
+    one-GPU box), config B plus the IMIX leg, each rank its own shard (weak scaling), and the
+    strong-scaling leg: one B and one C batch split into the two ranks' contiguous shards."""
     env = dict(os.environ, UPE_BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
            "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-hbm-probe",
-           "--max-copies", "24", "--imix-copies", "8"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+           "--max-copies", "24", "--imix-copies", "8", "--imix-v6fwd", "0"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -113,4 +115,8 @@ def test_bench_two_ranks():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["value"] > 0 and d["imix"]["value"] > 0
     assert "x2" in d["config"]["parallelism"]
+    for k in ("B", "C"):
+        st = d["strong"][k]
+        assert st["scaling"] == "strong" and st["value"] > 0
+        assert st["packets_per_step"] == 1 << 20 and st["packets_this_rank"] == 1 << 19
     print(json.dumps({k: d[k] for k in ("value", "ms_per_step", "n_gpus")}))
