@@ -270,16 +270,23 @@ int upe_gpu_process(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_des
  *   b[0..11]  bytes 0..11 of the forwarded frame (the original MACs when the lookup missed)
  *   b[12]     new TTL (IPv4) or hop limit (IPv6)
  *   b[13..14] new IPv4 header checksum as stored at frame bytes 24..25 (0 for IPv6)
- *   b[15]     4 or 6: the packet was forwarded (verdict code UPE_V_FWD) as that family;
- *             0 for every other verdict (the record is then all zero)
+ *   b[15]     4 or 6: the packet was forwarded (verdict code UPE_V_FWD) as that family
  * upe_hdr_apply(frame, rec) turns a frame into exactly the bytes process_packet leaves in
- * b->data; it does nothing when b[15] == 0. */
+ * b->data; it does nothing when b[15] == 0.
+ *
+ * Layout of a launch's records (round 5): only forwarded packets get one, compacted per 64-packet
+ * group in packet order — forwarded packet i's record is rec[64 * (i / 64) + k], k = the number
+ * of forwarded packets before it among packets 64 * (i / 64) .. i - 1 (the kernel's ballot and
+ * lane count; a reader walking the verdicts in order keeps a cursor, reset to i at every multiple
+ * of 64).  The other slots are not written.  UPE_HDR_SLOT gives the slot from that count. */
+#define UPE_HDR_SLOT(i, k) ((((size_t)(i)) & ~(size_t)63) + (size_t)(k))
 typedef struct {
     uint8_t b[16];
 } upe_hdr_rec_t;
 
-/* upe_gpu_process() in emit mode: d_hdr[i] (device, n records, 16-byte aligned) receives packet
- * i's rewritten header bytes and the frames are not written — except the ARP requests answered
+/* upe_gpu_process() in emit mode: d_hdr (device, room for n records, 16-byte aligned) receives
+ * the forwarded packets' rewritten header bytes (the record layout above) and the frames are not
+ * written — except the ARP requests answered
  * in place (UPE_VF_ARP_REPLY), which the reference transmits at once (src/worker.c:40-52).
  * Verdicts, counters, rule_stats and the L1 state are exactly those of upe_gpu_process().  This
  * is the layout for a TX path that sends header and payload as separate pieces (sendmmsg
@@ -295,8 +302,9 @@ int upe_gpu_process_emit(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *
  * persistent launch in emit mode, so the per-launch cost (dispatch, the first windows' round
  * trip, the tail, the boundary) is paid once per ring, not once per batch.  Counters,
  * rule_stats, the L1 state, every verdict code and every record equal those of `count`
- * back-to-back upe_gpu_process_emit() calls over the batches; UPE_VF_L1_INIT is relative to the
- * ring's start.  n a multiple of 1024, n * count <= 2^24.  d_done_ns (optional, device or
+ * back-to-back upe_gpu_process_emit() calls over the batches (record slots are counted from the
+ * ring's first packet; n is a multiple of 64, so each batch's records stay in its own range);
+ * UPE_VF_L1_INIT is relative to the ring's start.  n a multiple of 1024, n * count <= 2^24.  d_done_ns (optional, device or
  * host-mapped, count entries): for each batch, the time (ns) from the launch's first workgroup
  * to the moment its last workgroup had issued the batch's last stores — per-batch completion
  * latency — or 0 where not stamped (stamps need a linear-scan table, batches of at least
@@ -331,7 +339,8 @@ int upe_gpu_process_host(upe_gpu_ctx_t *ctx, uint8_t *h_frames, size_t frames_by
                          const uint64_t *h_desc, uint32_t *h_verdict, size_t n, size_t chunk);
 
 /* The host round trip in emit mode (chunk 0 = 128k packets): the same pipeline, but only the verdicts and the 16-byte
- * rewritten-header records come back (h_hdr, n records, pinned for the full rate: 20 bytes per
+ * rewritten-header records come back (h_hdr, room for n records in the layout above, counted
+ * from the batch's first packet; chunks are whole 64-packet groups; pinned for the full rate: 20 bytes per
  * packet over the link instead of the frames' rewritten span — the link's two directions share
  * its bandwidth, so fewer bytes back let the frames go in faster).  apply_threads >= 0: the
  * records are applied to h_frames on the host (upe_hdr_apply, answered ARP requests copied back)

@@ -60,7 +60,7 @@ def _mapped_run(w, wl, emit: bool, registered: bool = False):
             for i in np.nonzero(verdict & np.uint32(0x40))[0]:
                 replies[offs[i]:offs[i] + 96] = True
             assert not (changed & ~replies).any(), "emit mode wrote into non-reply frames"
-            frames = gpu.hdr_apply(frames, wl.desc, h.copy())
+            frames = gpu.hdr_apply(frames, wl.desc, gpu.expand_records(h.copy(), verdict))
         counters, stats = w.get_stats()
         return frames, verdict, counters, stats, w.get_l1()
     finally:

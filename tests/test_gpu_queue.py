@@ -143,6 +143,7 @@ def test_queue_shared_outputs(gpu_worker_factory):
             rec = np.empty((n, 16), np.uint8)
             w.d2h(rec, hdr)
             w.sync()
+            rec = gpu.expand_records(rec, verdict)   # (compacted per 64-packet group)
             counters, stats = w.get_stats()
             res.append((verdict, rec, counters.tobytes(), stats.copy(), w.get_l1().tobytes()))
             w.free(hdr)

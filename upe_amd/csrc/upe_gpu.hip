@@ -363,7 +363,8 @@ struct Args {
     uint32_t ntiles;                 // tiles of tw chunks
     unsigned long long* agree_out;   // host-mapped: (launch + 1) << 2 | start-state agreement bits
     unsigned long long launch_tag;   // this launch's index + 1
-    uint32_t* defer;                 // deferred look-back candidates: index | family << 31
+    uint32_t* defer;                 // deferred look-back candidates: (index | family << 31,
+                                     // record slot) pairs
     uint32_t lb_spin;                // longest look-back wait, 100 MHz ticks (then defer)
     // ring launch (upe_gpu_process_ring_emit): batches of ring_cpb chunks each; per batch the
     // workgroups that have finished it, and the clock (10 ns) at which the last one did,
@@ -1292,7 +1293,7 @@ template <bool kEmit>
 __device__ void repair_deferred(const Args& a, uint32_t nd, int lane, Repair m) {
     const uint32_t nchunks = (a.n + 63u) / 64u;
     uint32_t last = 0;   // the highest chunk with a deferred candidate: F beyond it does not matter
-    for (uint32_t e = lane; e < nd; e += 64) last = max(last, (a.defer[e] & 0x7FFFFFFFu) / 64u);
+    for (uint32_t e = lane; e < nd; e += 64) last = max(last, (a.defer[2 * e] & 0x7FFFFFFFu) / 64u);
     last = wave_reduce<2>(last);
     uint32_t F4 = kNone, F6 = kNone;
     for (uint32_t b = 0; b <= last && b < nchunks && (F4 == kNone || F6 == kNone); b += 64) {
@@ -1312,13 +1313,14 @@ __device__ void repair_deferred(const Args& a, uint32_t nd, int lane, Repair m) 
     // kRepairUnroll entries per lane at a time, their loads issued together (one wave does this)
     constexpr int U = kRepairUnroll;
     for (uint32_t e0 = 0; e0 < nd; e0 += U * 64) {
-        uint32_t x[U], v[U];
+        uint32_t x[U], v[U], rs[U];
         uint4 q[U];
         bool p[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint32_t e = e0 + 64u * k + (uint32_t)lane;
-            x[k] = e < nd ? a.defer[e] : kNone;
+            x[k] = e < nd ? a.defer[2 * e] : kNone;
+            rs[k] = e < nd ? a.defer[2 * e + 1] : 0u;   // the record slot (emit mode)
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -1328,7 +1330,7 @@ __device__ void repair_deferred(const Args& a, uint32_t nd, int lane, Repair m) 
             p[k] = x[k] != kNone && (v6 ? F6 : F4) >= i / 64u;
             if (p[k]) {
                 v[k] = a.verdict[i];
-                q[k] = kEmit ? a.hdr[i]
+                q[k] = kEmit ? a.hdr[rs[k]]
                              : *reinterpret_cast<const uint4*>(a.frames + ((size_t)(a.desc[i] >> 20) << 4));
             }
         }
@@ -1340,7 +1342,7 @@ __device__ void repair_deferred(const Args& a, uint32_t nd, int lane, Repair m) 
             a.verdict[i] = v[k] | UPE_VF_NEIGH_HIT;
             const uint4 o = make_uint4(v6 ? m.mac6_lo : m.mac4_lo, v6 ? w1_6 : w1_4, w2, q[k].w);
             if (kEmit)
-                a.hdr[i] = o;
+                a.hdr[rs[k]] = o;
             else
                 *reinterpret_cast<uint4*>(a.frames + ((size_t)(a.desc[i] >> 20) << 4)) = o;
         }
@@ -1813,6 +1815,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             }
             if (cand) flags |= UPE_VF_L1_INIT;
         }
+        // emit mode: a record for each forwarded packet only, compacted per 64-packet group in
+        // packet order (the wave's chunk is one group): a ballot and a lane count give its slot,
+        // 64 * (i / 64) + the forwarded packets before it in the group.  No record is written for
+        // the other packets (config B: 7.5 MB of zero records per 1M batch before round 5).
+        uint32_t rslot = 0;
+        if (kEmit) {
+            const unsigned long long fm = __ballot(live && code == UPE_V_FWD);
+            rslot = ch * 64u + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        }
         if (kNoLB) {
             // a disagreeing entry here belongs to a family whose index is empty
             if (cand && (r.v6 ? look6 : look4)) {
@@ -1877,7 +1889,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                         if (dm) base = atomicAdd(&acc_cur(a)->ndefer, (uint32_t)__popcll(dm));
                     }
                     base = __builtin_amdgcn_readfirstlane(base);
-                    if (dl) a.defer[base + (uint32_t)__popcll(dm & lt)] = i | (r.v6 ? 0x80000000u : 0u);
+                    if (dl) {   // (index | family, and the packet's record slot in emit mode)
+                        const uint32_t e = base + (uint32_t)__popcll(dm & lt);
+                        a.defer[2 * e] = i | (r.v6 ? 0x80000000u : 0u);
+                        a.defer[2 * e + 1] = rslot;
+                    }
                     deferred = dm != 0;
                 }
             }
@@ -1885,24 +1901,22 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (hit) flags |= UPE_VF_NEIGH_HIT;
 
         // ---- write back ----
-        if (kEmit && live && !(kAblate & 8)) {
+        if (kEmit && live && code == UPE_V_FWD && !(kAblate & 8)) {
             // record: bytes 0..11 as forwarded (neighbour + port MAC on a hit, else unchanged),
-            // the new TTL / hop limit, the new IPv4 checksum, the family; zero unless forwarded
-            uint4 rec = make_uint4(0, 0, 0, 0);
-            if (code == UPE_V_FWD) {
-                rec.x = hit ? mlo : w[0];
-                rec.y = hit ? (mhi | (a.port_mac_lo << 16)) : w[1];
-                rec.z = hit ? ((a.port_mac_lo >> 16) | (a.port_mac_hi << 16)) : w[2];
-                rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
-                             : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
-            }
+            // the new TTL / hop limit, the new IPv4 checksum, the family
+            uint4 rec;
+            rec.x = hit ? mlo : w[0];
+            rec.y = hit ? (mhi | (a.port_mac_lo << 16)) : w[1];
+            rec.z = hit ? ((a.port_mac_lo >> 16) | (a.port_mac_hi << 16)) : w[2];
+            rec.w = r.v6 ? (((r.c1w1 >> 8) & 0xFFu) | (6u << 24))
+                         : (((r.c1w1 >> 16) & 0xFFu) | ((r.c1w2 & 0xFFFFu) << 8) | (4u << 24));
             {   // a buffer store with the write-through cache policy (kRecAux)
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.hdr, 0, 0x7FFFFFF0, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(v4u{rec.x, rec.y, rec.z, rec.w}, rs, i * 16u, 0,
-                                                       kRecAux);
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{rec.x, rec.y, rec.z, rec.w}, rs,
+                                                       rslot * 16u, 0, kRecAux);
             }
-        } else if (live && !(kAblate & 8)) {
+        } else if (!kEmit && live && !(kAblate & 8)) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
                 store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
@@ -2639,7 +2653,7 @@ int ensure_scratch(upe_gpu_ctx* c, size_t ntiles) {
         size_t want = ntiles + ntiles / 4 + 16;
         HIP_TRY(hipMalloc(&c->lb, want * kWaves * sizeof(uint32_t)));
         HIP_TRY(hipMemset(c->lb, 0, want * kWaves * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&c->defer, 64 * want * kWaves * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&c->defer, 2 * 64 * want * kWaves * sizeof(uint32_t)));
         c->tiles_alloc = want;
         if (publish(c) != 0) return -1;
     }
@@ -4344,6 +4358,9 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
     // default chunks (round-3 sweep, config B 1M): in place 256k (479 Mpps; 128k 406, 64k 359),
     // emit 128k (559 Mpps; 256k 534, 64k 529)
     if (chunk == 0) chunk = emit ? (size_t)1 << 17 : (size_t)1 << 18;
+    // emit: whole 64-packet groups per chunk, so that each chunk's compacted records (relative to
+    // its first packet) land where the batch's own layout puts them
+    if (emit) chunk = std::max<size_t>(64, chunk & ~(size_t)63);
     if (!c->s_in) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
@@ -4395,9 +4412,16 @@ int host_roundtrip(upe_gpu_ctx_t* c, uint8_t* h_frames, size_t frames_bytes,
         auto job = [&](unsigned t, unsigned T) {
             const size_t m = d.e - d.s, a0 = d.s + m * t / T, a1 = d.s + m * (t + 1) / T;
             bool r = false;
+            // the compacted record of the range's first forwarded packet
+            size_t rec = a0 & ~(size_t)63;
+            for (size_t j = rec; j < a0; ++j) rec += UPE_VERDICT_CODE(h_verdict[j]) == UPE_V_FWD;
             for (size_t i = a0; i < a1; ++i) {
                 r |= (h_verdict[i] & UPE_VF_ARP_REPLY) != 0;
-                if (apply && h_hdr[i].b[15]) upe_hdr_apply(h_frames + (h_desc[i] >> 16), &h_hdr[i]);
+                if ((i & 63u) == 0) rec = i;
+                if (UPE_VERDICT_CODE(h_verdict[i]) == UPE_V_FWD) {
+                    if (apply) upe_hdr_apply(h_frames + (h_desc[i] >> 16), &h_hdr[rec]);
+                    ++rec;
+                }
             }
             if (r) replies.store(true, std::memory_order_relaxed);
         };

@@ -171,6 +171,7 @@ static int walk(loop_t *L, int k) {
     slot_t *S = &L->s[k];
     if (upe_gpu_mark_wait(L->ctx, k) != 0) return -1;
     const size_t n = S->n;
+    size_t rec = 0; /* window mode: the next forwarded packet's record (compacted per 64) */
     for (size_t i = 0; i < n; i++) {
         void *b = S->bufs[i];
         uint8_t *d = S->data[i];
@@ -180,8 +181,9 @@ static int walk(loop_t *L, int k) {
         if (!L->pool) {
             /* window mode: the rewritten bytes into the caller's buffer (an answered ARP
              * request ends a cut batch, so nothing is queued behind it: a synchronous copy) */
+            if ((i & 63u) == 0) rec = i;
             if (code == UPE_V_FWD) {
-                upe_hdr_apply(d, &S->rec[i]);
+                upe_hdr_apply(d, &S->rec[rec++]);
             } else if (v & UPE_VF_ARP_REPLY) {
                 const size_t c = len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT;
                 if (upe_gpu_memcpy_d2h(L->ctx, d, S->d_win + i * WIN, c, NULL) != 0 ||

@@ -636,20 +636,51 @@ class DeviceBatch:
         self.worker.sync()
         return frames, verdict
 
-    def fetch_hdr(self) -> np.ndarray:
-        """The emit-mode records, (n, 16) uint8 (synchronises)."""
+    def fetch_hdr(self, raw: bool = False) -> np.ndarray:
+        """The emit-mode records (synchronises): one per packet, (n, 16) uint8, zero for a packet
+        not forwarded (expand_records); raw=True: the device array as the kernel left it (records
+        of forwarded packets compacted per 64-packet group, the other slots unwritten)."""
         self.worker.sync()
-        rec = np.empty((self.n, 16), np.uint8)
+        rec = np.zeros((self.n, 16), np.uint8)
+        verdict = np.empty(self.n, np.uint32)
         if self.n:
             self.worker.d2h(rec, self.hdr)
+            self.worker.d2h(verdict, self.verdict)
         self.worker.sync()
-        return rec
+        return rec if raw else expand_records(rec, verdict)
 
     def free(self) -> None:
         for p in (self.frames, self.desc, self.verdict, self.hdr):
             if p:
                 self.worker.free(p)
         self.frames = self.desc = self.verdict = self.hdr = 0
+
+
+def record_slots(verdict: np.ndarray) -> np.ndarray:
+    """Emit mode's record layout (include/upe_gpu.h): forwarded packet i's record sits at
+    64 * (i // 64) + the number of forwarded packets before it in its 64-packet group.  Returns
+    that slot for every packet (meaningful for forwarded ones)."""
+    from .layout import V_FWD
+
+    v = np.asarray(verdict, np.uint32)
+    fwd = ((v & 0xF) == V_FWD).astype(np.int64)
+    excl = np.cumsum(fwd) - fwd
+    idx = np.arange(len(v), dtype=np.int64)
+    grp = idx & ~np.int64(63)
+    return grp + excl - excl[grp] if len(v) else idx
+
+
+def expand_records(rec_raw: np.ndarray, verdict: np.ndarray) -> np.ndarray:
+    """Per-packet records, (n, 16) uint8, zero for packets not forwarded, from the compacted
+    array the emit-mode kernel writes (record_slots)."""
+    from .layout import V_FWD
+
+    raw = np.ascontiguousarray(rec_raw, np.uint8).reshape(-1, 16)
+    v = np.asarray(verdict, np.uint32)
+    out = np.zeros((len(v), 16), np.uint8)
+    fwd = (v & 0xF) == V_FWD
+    out[fwd] = raw[record_slots(v)[fwd]]
+    return out
 
 
 def hdr_apply(frames: np.ndarray, desc: np.ndarray, rec: np.ndarray) -> np.ndarray:
