@@ -3501,23 +3501,6 @@ uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
     return best;
 }
 
-int upload_bytes(void** dst, const void* src, size_t bytes) {
-    if (*dst) (void)hipFree(*dst);
-    *dst = nullptr;
-    if (bytes == 0) return 0;
-    HIP_TRY(hipMalloc(dst, bytes));
-    HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
-    return 0;
-}
-int upload(TssGroup*& dst, const std::vector<TssGroup>& v) {
-    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(TssGroup));
-}
-int upload(uint4*& dst, const std::vector<uint4>& v) {
-    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint4));
-}
-int upload(uint16_t*& dst, const std::vector<uint16_t>& v) {
-    return upload_bytes(reinterpret_cast<void**>(&dst), v.data(), v.size() * sizeof(uint16_t));
-}
 // rule_t -> the compiled words: RuleV4 / RuleV6 (pre-masked) and rinfo, pad >= count entries (the
 // padding never matches).  -1 (message set) on a rule_id outside [0, cap).
 int compile_rules(const upe_rule_t* rules, size_t count, size_t cap, size_t pad,
@@ -3605,85 +3588,90 @@ size_t tree_node_budget(size_t count) {
 }  // namespace
 extern "C" {
 
-extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count) {
-    if (!c) return fail("null context");
-    if (count > c->cap) return fail("rule count exceeds the capacity given at open");
-    if (count && !rules) return fail("null rules");
-    DEV_SCOPE(c->device);
+}  // extern "C"
+
+namespace {
+// A device allocation that frees itself unless taken: load_rules uploads every image of the new
+// table first and changes the context only once all of them are on the device.
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int put(const void* src, size_t bytes) {
+        if (bytes == 0) return 0;
+        HIP_TRY(hipMalloc(&p, bytes));
+        HIP_TRY(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+        return 0;
+    }
+    template <class T>
+    T* take() {
+        T* q = static_cast<T*>(p);
+        p = nullptr;
+        return q;
+    }
+};
+template <class T>
+void replace(T*& field, DevBuf& b) {
+    if (field) (void)hipFree(field);
+    field = b.take<T>();
+}
+
+// upe_gpu_load_rules, and upe_gpu_reload_rules with `fresh` (a zeroed rule_stats of fresh_cap
+// entries that replaces the context's, the old per-index totals dropped instead of credited).
+// Everything the new table needs is built and uploaded before the context changes: on an error
+// the context keeps classifying with the old table and its statistics.
+int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
+                    DevBuf* fresh, size_t fresh_cap) {
+    const size_t cap = fresh ? fresh_cap : c->cap;
     const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
     std::vector<RuleV4> v4;
     std::vector<RuleV6> v6;
     std::vector<int2> info;
-    if (compile_rules(rules, count, c->cap, pad, v4, v6, info) != 0) return -1;
-    // previous batches may still read the table, on whichever stream they went
-    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (fold_stats_idx(c) != 0) return -1;
-    if (pad > c->rules_alloc) {
-        if (c->rv4) (void)hipFree(c->rv4);
-        if (c->rv6) (void)hipFree(c->rv6);
-        if (c->rinfo) (void)hipFree(c->rinfo);
-        c->rv4 = nullptr; c->rv6 = nullptr; c->rinfo = nullptr;
-        c->rules_alloc = 0;
-        HIP_TRY(hipMalloc(&c->rv4, pad * sizeof(RuleV4)));
-        HIP_TRY(hipMalloc(&c->rv6, pad * sizeof(RuleV6)));
-        HIP_TRY(hipMalloc(&c->rinfo, pad * sizeof(int2)));
-        if (c->stats_idx) (void)hipFree(c->stats_idx);
-        c->stats_idx = nullptr;
-        HIP_TRY(hipMalloc(&c->stats_idx, pad * 2 * kStatReps * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(c->stats_idx, 0, pad * 2 * kStatReps * sizeof(unsigned long long)));
-        c->rules_alloc = pad;
-        if (publish(c) != 0) return -1;
-    }
-    HIP_TRY(hipMemcpy(c->rv4, v4.data(), pad * sizeof(RuleV4), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->rv6, v6.data(), pad * sizeof(RuleV6), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->rinfo, info.data(), pad * sizeof(int2), hipMemcpyHostToDevice));
-    // linear-scan tables past the LDS copy: the per-family lists (FamTable)
+    if (compile_rules(rules, count, cap, pad, v4, v6, info) != 0) return -1;
     // a family none of whose reachable rules forwards never consults or updates its L1 entry
     // (src/worker.c:155-244 run only for forwarded packets): its entry's agreement is moot
+    bool fwd4 = false, fwd6 = false;
     {
         bool e4 = false, e6 = false;
-        c->fwd4 = c->fwd6 = false;
         for (size_t i = 0; i < count && !(e4 && e6); ++i) {
             const uint8_t ver = rules[i].ip_ver;
             const bool all4 = matches_all4(v4[i]), all6 = matches_all6(v4[i], v6[i]);
             const bool fwd = rules[i].action.type == UPE_ACT_FWD;
-            if (!e4 && (ver == 0 || ver == 4)) { c->fwd4 = c->fwd4 || fwd; e4 = all4; }
-            if (!e6 && (ver == 0 || ver == 6)) { c->fwd6 = c->fwd6 || fwd; e6 = all6; }
+            if (!e4 && (ver == 0 || ver == 4)) { fwd4 = fwd4 || fwd; e4 = all4; }
+            if (!e6 && (ver == 0 || ver == 6)) { fwd6 = fwd6 || fwd; e6 = all6; }
         }
-        // the kernel without look-back may have been chosen because a family could not forward
-        // under the old table: back to the full kernel until a launch under this one reports
-        c->no_lb = false;
-        c->lb_reset_k = c->k;
     }
-    c->fam4 = c->fam6 = 0;
-    c->fam_all = 0;
-    c->fam_x1idx = 0;
+    // linear-scan tables past the LDS copy: the per-family lists (FamTable)
+    uint32_t fam4 = 0, fam6 = 0, fam_all = 0, fam_x1idx = 0;
     std::vector<uint32_t> l4, l6;   // the family lists' sorted indexes
+    std::vector<uint4> fimg;
     if (pad > (size_t)kSmallRules) {
         bool end4 = false, end6 = false;
         family_lists(rules, count, v4, v6, l4, l6, end4, end6);
         const size_t n4 = (l4.size() + kUnroll - 1) / kUnroll * kUnroll;
         const size_t n6 = (l6.size() + kUnroll - 1) / kUnroll * kUnroll;
         // (+1: the scalar scan loads an IPv6 entry's last 48 bytes as 64)
-        std::vector<uint4> img(2 * n4 + kFamV6Stride * n6 + (n4 + n6 + 3) / 4 + 1);
-        memset(img.data(), 0, img.size() * sizeof(uint4));
+        fimg.assign(2 * n4 + kFamV6Stride * n6 + (n4 + n6 + 3) / 4 + 1, make_uint4(0, 0, 0, 0));
         RuleV4 never;
         memset(&never, 0, sizeof never);
         never.x0 = 0xFF;   // ip_ver byte 0xFF against a key version of 4 or 6
         never.m0 = 0xFF;
-        uint32_t* idx = reinterpret_cast<uint32_t*>(img.data() + 2 * n4 + kFamV6Stride * n6);
+        uint32_t* idx = reinterpret_cast<uint32_t*>(fimg.data() + 2 * n4 + kFamV6Stride * n6);
         // tables below 8192 rules: the sorted index rides in x1 bits 18-30 (m1 keeps them clear,
         // so the match is unchanged) and comes back with the matched rule's words
         const bool x1idx = count < 8192;
         for (size_t j = 0; j < n4; ++j) {
             RuleV4 e = j < l4.size() ? v4[l4[j]] : never;
             if (x1idx && j < l4.size()) e.x1 |= l4[j] << 18;
-            memcpy(&img[2 * j], &e, sizeof e);
+            memcpy(&fimg[2 * j], &e, sizeof e);
             idx[j] = j < l4.size() ? l4[j] : 0u;
         }
         for (size_t j = 0; j < n6; ++j) {
-            uint4* o = &img[2 * n4 + kFamV6Stride * j];
+            uint4* o = &fimg[2 * n4 + kFamV6Stride * j];
             if (j < l6.size()) {
                 RuleV4 e = v4[l6[j]];
                 if (x1idx) e.x1 |= l6[j] << 18;
@@ -3694,86 +3682,144 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
             }
             idx[n4 + j] = j < l6.size() ? l6[j] : 0u;
         }
-        const size_t bytes = img.size() * sizeof(uint4);
-        if (bytes > c->fam_alloc) {
-            if (c->fam) (void)hipFree(c->fam);
-            c->fam = nullptr;
-            c->fam_alloc = 0;
-            HIP_TRY(hipMalloc(&c->fam, bytes));
-            c->fam_alloc = bytes;
-        }
-        HIP_TRY(hipMemcpy(c->fam, img.data(), bytes, hipMemcpyHostToDevice));
-        c->fam4 = (uint32_t)n4;
-        c->fam6 = (uint32_t)n6;
-        c->fam_all = (l4.size() == 1 && end4 ? 1u : 0u) | (l6.size() == 1 && end6 ? 2u : 0u);
-        c->fam_x1idx = x1idx ? 1u : 0u;
+        fam4 = (uint32_t)n4;
+        fam6 = (uint32_t)n6;
+        fam_all = (l4.size() == 1 && end4 ? 1u : 0u) | (l6.size() == 1 && end6 ? 2u : 0u);
+        fam_x1idx = x1idx ? 1u : 0u;
     }
-    c->nrules = (uint32_t)count;
-    c->nrules_pad = (uint32_t)pad;
-    c->rinfo_host = info;
-
     // Large tables: a tuple-space index when the rules fall into few mask signatures (one hash
-    // probe per signature instead of a test per rule); otherwise the linear scan.
-    c->tss = false;
-    c->nfs = 0;
-    c->ng4 = c->ng6 = 0;
+    // probe per signature instead of a test per rule).
+    bool tss = false;
+    TssFamily f4, f6;
+    std::vector<uint16_t> fps;   // the staged fingerprint image
     const char* force = getenv("UPE_GPU_TSS");   // diagnostic: 0 = never, 1 = always
-    if (count > 0 && count < kTssMaxRules && !(force && force[0] == '0')) {
-        TssFamily f4, f6;
-        if (build_tss_family(4, v4, v6, rules, count, f4) &&
-            build_tss_family(6, v4, v6, rules, count, f6)) {
-            const size_t ng = f4.groups.size() + f6.groups.size();
-            if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
-                // the staged fingerprint image: small groups, in probe order, while it fits
-                std::vector<uint16_t> img;
-                const char* fps = getenv("UPE_GPU_FP_STAGE");   // diagnostic: 0 = stage none
-                for (TssFamily* f : {&f4, &f6})
-                    for (TssGroup& g : f->groups) {
-                        if (fps && fps[0] == '0') break;
-                        const uint32_t slots = 1u << g.w[11];
-                        if ((g.w[14] & 1u) || slots > kFpStageGroup || img.size() + slots > kFpStageMax)
-                            continue;
-                        g.w[15] = 1u + (uint32_t)img.size();
-                        img.insert(img.end(), f->fp.begin() + g.w[13], f->fp.begin() + g.w[13] + slots);
-                    }
-                img.resize((img.size() + 7) & ~(size_t)7, 0);
-                if (upload(c->tfs, img)) return -1;
-                c->nfs = (uint32_t)(img.size() / 8);
-                if (upload(c->tg4, f4.groups) || upload(c->tg6, f6.groups) ||
-                    upload(c->tt4, f4.slots) || upload(c->tt6, f6.slots))
-                    return -1;
-                c->ng4 = (uint32_t)f4.groups.size();
-                c->ng6 = (uint32_t)f6.groups.size();
-                c->tss = true;
-            }
+    if (count > 0 && count < kTssMaxRules && !(force && force[0] == '0') &&
+        build_tss_family(4, v4, v6, rules, count, f4) && build_tss_family(6, v4, v6, rules, count, f6)) {
+        const size_t ng = f4.groups.size() + f6.groups.size();
+        if ((force && force[0] == '1') || (count >= 1024 && ng * 16 <= count)) {
+            // the staged fingerprint image: small groups, in probe order, while it fits
+            const char* st = getenv("UPE_GPU_FP_STAGE");   // diagnostic: 0 = stage none
+            for (TssFamily* f : {&f4, &f6})
+                for (TssGroup& g : f->groups) {
+                    if (st && st[0] == '0') break;
+                    const uint32_t slots = 1u << g.w[11];
+                    if ((g.w[14] & 1u) || slots > kFpStageGroup || fps.size() + slots > kFpStageMax)
+                        continue;
+                    g.w[15] = 1u + (uint32_t)fps.size();
+                    fps.insert(fps.end(), f->fp.begin() + g.w[13], f->fp.begin() + g.w[13] + slots);
+                }
+            fps.resize((fps.size() + 7) & ~(size_t)7, 0);
+            tss = true;
         }
     }
     // Linear-scan tables past kSmallRules without a tuple-space index: the decision tree over the
     // family lists (kTreeDims comment), unless it outgrows its node budget (UPE_GPU_TREE: 0 = never,
     // diagnostic; UPE_GPU_TREE_BINTH: rules per leaf before a split)
-    c->tree_ok = false;
+    bool tree_ok = false;
+    std::vector<uint4> timg;
+    TreeImage t;
     const char* tf = getenv("UPE_GPU_TREE");
-    const char* tl = getenv("UPE_GPU_TREE_LDS");   // diagnostic: 0 = the image stays in memory
-    c->tree_stage = !(tl && tl[0] == '0');
-    if (!c->tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0')) {
+    if (!tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0')) {
         const char* bt = getenv("UPE_GPU_TREE_BINTH");
         const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : kTreeBinth;
-        TreeImage t;
         if (build_tree(v4, v6, l4, l6, binth, tree_node_budget(count), t)) {
             const size_t nw = 2 * t.nodes.size() + t.leaves.size();
-            std::vector<uint4> img((nw + 3) / 4, make_uint4(0, 0, 0, 0));
-            memcpy(img.data(), t.nodes.data(), t.nodes.size() * sizeof(uint2));
-            memcpy(reinterpret_cast<uint32_t*>(img.data()) + 2 * t.nodes.size(), t.leaves.data(),
+            timg.assign((nw + 3) / 4, make_uint4(0, 0, 0, 0));
+            memcpy(timg.data(), t.nodes.data(), t.nodes.size() * sizeof(uint2));
+            memcpy(reinterpret_cast<uint32_t*>(timg.data()) + 2 * t.nodes.size(), t.leaves.data(),
                    t.leaves.size() * sizeof(uint32_t));
-            if (upload(c->tree, img)) return -1;
-            c->tree_words = (uint32_t)img.size();
-            c->tree_loff = (uint32_t)(2 * t.nodes.size());
-            c->tree_info = {(uint64_t)t.nodes.size(), (uint64_t)t.leaves.size(), t.depth[0],
-                            t.depth[1], t.max_leaf, t.trees[0] | t.trees[1] << 16};
-            c->tree_ok = true;
+            tree_ok = true;
         }
     }
-    return 0;
+
+    // every image on the device before anything of the context changes
+    DevBuf b_rv4, b_rv6, b_rinfo, b_idx, b_fam, b_tfs, b_tg4, b_tg6, b_tt4, b_tt6, b_tree;
+    if (b_rv4.put(v4.data(), pad * sizeof(RuleV4)) || b_rv6.put(v6.data(), pad * sizeof(RuleV6)) ||
+        b_rinfo.put(info.data(), pad * sizeof(int2)) ||
+        b_fam.put(fimg.data(), fimg.size() * sizeof(uint4)) ||
+        (tss && (b_tfs.put(fps.data(), fps.size() * sizeof(uint16_t)) ||
+                 b_tg4.put(f4.groups.data(), f4.groups.size() * sizeof(TssGroup)) ||
+                 b_tg6.put(f6.groups.data(), f6.groups.size() * sizeof(TssGroup)) ||
+                 b_tt4.put(f4.slots.data(), f4.slots.size() * sizeof(uint4)) ||
+                 b_tt6.put(f6.slots.data(), f6.slots.size() * sizeof(uint4)))) ||
+        (tree_ok && b_tree.put(timg.data(), timg.size() * sizeof(uint4))))
+        return -1;
+    const bool grow = pad > c->rules_alloc;
+    if (grow) {
+        const size_t bytes = pad * 2 * kStatReps * sizeof(unsigned long long);
+        HIP_TRY(hipMalloc(&b_idx.p, bytes));
+        HIP_TRY(hipMemset(b_idx.p, 0, bytes));
+    }
+    // previous batches may still read the table, on whichever stream they went
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (fresh) {
+        // the reload's fresh statistics: the old table's per-index totals are dropped
+        if (c->stats_idx)
+            HIP_TRY(hipMemset(c->stats_idx, 0,
+                              (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats)));
+        if (c->stats) (void)hipFree(c->stats);
+        c->stats = fresh->take<unsigned long long>();
+        c->cap = fresh_cap;
+        c->rinfo_host.clear();
+    } else if (fold_stats_idx(c) != 0) {   // the old table's counts credited to their rule_ids
+        return -1;
+    }
+    // the swap
+    replace(c->rv4, b_rv4);
+    replace(c->rv6, b_rv6);
+    replace(c->rinfo, b_rinfo);
+    if (grow) {
+        replace(c->stats_idx, b_idx);
+        c->rules_alloc = pad;
+    }
+    replace(c->fam, b_fam);
+    c->fam_alloc = fimg.size() * sizeof(uint4);
+    c->fam4 = fam4;
+    c->fam6 = fam6;
+    c->fam_all = fam_all;
+    c->fam_x1idx = fam_x1idx;
+    c->fwd4 = fwd4;
+    c->fwd6 = fwd6;
+    // the kernel without look-back may have been chosen because a family could not forward
+    // under the old table: back to the full kernel until a launch under this one reports
+    c->no_lb = false;
+    c->lb_reset_k = c->k;
+    c->nrules = (uint32_t)count;
+    c->nrules_pad = (uint32_t)pad;
+    c->rinfo_host = info;
+    replace(c->tfs, b_tfs);
+    replace(c->tg4, b_tg4);
+    replace(c->tg6, b_tg6);
+    replace(c->tt4, b_tt4);
+    replace(c->tt6, b_tt6);
+    c->tss = tss;
+    c->nfs = tss ? (uint32_t)(fps.size() / 8) : 0u;
+    c->ng4 = tss ? (uint32_t)f4.groups.size() : 0u;
+    c->ng6 = tss ? (uint32_t)f6.groups.size() : 0u;
+    replace(c->tree, b_tree);
+    c->tree_ok = tree_ok;
+    const char* tl = getenv("UPE_GPU_TREE_LDS");   // diagnostic: 0 = the image stays in memory
+    c->tree_stage = !(tl && tl[0] == '0');
+    c->tree_words = tree_ok ? (uint32_t)timg.size() : 0u;
+    c->tree_loff = tree_ok ? (uint32_t)(2 * t.nodes.size()) : 0u;
+    c->tree_info = tree_ok ? upe_rule_index_info_t{(uint64_t)t.nodes.size(), (uint64_t)t.leaves.size(),
+                                                   t.depth[0], t.depth[1], t.max_leaf,
+                                                   t.trees[0] | t.trees[1] << 16}
+                           : upe_rule_index_info_t{};
+    return publish(c);   // the DevState's pointers (stats, stats_idx)
+}
+}  // namespace
+
+extern "C" {
+
+extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count) {
+    if (!c) return fail("null context");
+    if (count > c->cap) return fail("rule count exceeds the capacity given at open");
+    if (count && !rules) return fail("null rules");
+    DEV_SCOPE(c->device);
+    return load_rules_impl(c, rules, count, nullptr, 0);
 }
 
 // The reference's SIGHUP reload (src/main.c:216-282): the stats thread builds a new table
@@ -3782,7 +3828,9 @@ extern "C" int upe_gpu_load_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, siz
 // frees the old ones after a grace period.  The worker's pkts_* counters and its one-entry L1
 // neighbour caches are untouched.  Here: the batches queued so far finish with the old table,
 // their rule_stats (credited to the old rule_ids) are handed back in old_stats if asked for,
-// and the next batch runs with the new table and an all-zero rule_stats[rule_capacity].
+// and the next batch runs with the new table and an all-zero rule_stats[rule_capacity].  All or
+// nothing: on an error the old table and its statistics stay (as the reference keeps both when
+// rule_config_load fails, src/main.c:229-255).
 extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
                                     size_t rule_capacity, upe_rule_stat_t* old_stats,
                                     size_t old_capacity) {
@@ -3798,23 +3846,10 @@ extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, s
     if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (old_capacity && read_rule_stats(c, old_stats, old_capacity) != 0) return -1;
-    // a fresh, zeroed rule_stats of the new capacity; the old table's per-index totals dropped
-    unsigned long long* fresh = nullptr;
-    HIP_TRY(hipMalloc(&fresh, rule_capacity * 2 * sizeof(unsigned long long)));
-    if (order_on(c, c->stream) != 0) return -1;
-    HIP_TRY(hipMemsetAsync(fresh, 0, rule_capacity * 2 * sizeof(unsigned long long), c->stream));
-    if (c->stats_idx)
-        HIP_TRY(hipMemsetAsync(c->stats_idx, 0,
-                               (size_t)c->rules_alloc * 2 * kStatReps * sizeof(unsigned long long),
-                               c->stream));
-    HIP_TRY(hipMemsetAsync(&c->st->acc_stats[0][0], 0, sizeof(c->st->acc_stats), c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->stats) (void)hipFree(c->stats);
-    c->stats = fresh;
-    c->cap = rule_capacity;
-    c->rinfo_host.clear();   // nothing of the old table is left to credit
-    if (publish(c) != 0) return -1;
-    return upe_gpu_load_rules(c, rules, count);
+    DevBuf fresh;   // a zeroed rule_stats of the new capacity (freed unless the reload succeeds)
+    HIP_TRY(hipMalloc(&fresh.p, rule_capacity * 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(fresh.p, 0, rule_capacity * 2 * sizeof(unsigned long long)));
+    return load_rules_impl(c, rules, count, &fresh, rule_capacity);
 }
 
 extern "C" int upe_gpu_rule_index_kind(upe_gpu_ctx_t* c) {
