@@ -399,72 +399,18 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
 /* =========================================================================================== */
 /* The reference's throughput benchmark with CPU or GPU workers                                 */
 /* =========================================================================================== */
-/* build_dummy_packet of reference tests/benchmark_throughput.c:138-175: Eth + IPv4 (TTL 64,
- * 10.128.0.1 -> 10.128.0.2) + TCP 45000 -> 80, zero padded to packet_size. */
-static void build_dummy_packet(pktbuf_t *b, int packet_size) {
-    b->len = (size_t)packet_size;
-    uint8_t *p = b->data;
-    memset(p, 0, (size_t)packet_size);
-    p[12] = 0x08;
-    p[13] = 0x00;
-    p += 14;
-    p[0] = 0x45;
-    p[2] = (uint8_t)((packet_size - 14) >> 8);
-    p[3] = (uint8_t)((packet_size - 14) & 0xFF);
-    p[8] = 64;
-    p[9] = 6;
-    p[12] = 10; p[13] = 128; p[14] = 0; p[15] = 1;
-    p[16] = 10; p[17] = 128; p[18] = 0; p[19] = 2;
-    p += 20;
-    p[0] = 0xAF; p[1] = 0xC8;
-    p[2] = 0x00; p[3] = 0x50;
-    p[12] = 0x50;
-}
-
-static double mono_s(void) {
-    struct timespec ts;
-    clock_gettime(CLOCK_MONOTONIC_RAW, &ts);
-    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
-}
-
-/* run_producer of reference tests/benchmark_throughput.c:188-238: allocate, build, push round
- * robin over the workers' rings, free what a full ring refuses; returns pushes, full events. */
-static void producer(pktbuf_pool_t *pool, spsc_ring_t *rings, int nw, int batch, int psize,
-                     double seconds, uint64_t *pushed, uint64_t *full, double *dur) {
-    void *b[256];
-    int ring_idx = 0, check = 0;
-    *pushed = *full = 0;
-    const double start = mono_s(), deadline = start + seconds;
-    double now = start;
-    while (now < deadline) {
-        int actual = 0;
-        for (int i = 0; i < batch; i++) {
-            pktbuf_t *p = pktbuf_alloc(pool);
-            if (!p) break;
-            build_dummy_packet(p, psize);
-            b[actual++] = p;
-        }
-        if (actual == 0) {
-            struct timespec ts = {0, 1000};
-            nanosleep(&ts, NULL);
-            now = mono_s();
-            check = 0;
-            continue;
-        }
-        unsigned pu = ring_push_burst(&rings[ring_idx], b, (unsigned)actual);
-        *pushed += pu;
-        if (pu < (unsigned)actual) {
-            (*full)++;
-            for (unsigned i = pu; i < (unsigned)actual; i++) pktbuf_free(pool, b[i]);
-        }
-        ring_idx = (ring_idx + 1) % nw;
-        if (++check >= 128) {
-            now = mono_s();
-            check = 0;
-        }
-    }
-    *dur = mono_s() - start;
-}
+/* The reference benchmark's own packet builder and producer (tests/benchmark_throughput.c:
+ * 138-238: build_dummy_packet, run_producer), included where they lie; its g_stop, TX stubs and
+ * main are renamed out of the way (this file defines the program's g_stop and logging stubs). */
+#define g_stop upe_refbench_g_stop
+#define tx_send upe_refbench_tx_send
+#define tx_send_batch upe_refbench_tx_send_batch
+#define main upe_refbench_main
+#include "benchmark_throughput.c"
+#undef g_stop
+#undef tx_send
+#undef tx_send_batch
+#undef main
 
 /*
  * The reference benchmark's setup (tests/benchmark_throughput.c:87-116: one TCP FWD rule, one ARP
@@ -540,12 +486,16 @@ int upe_dropin_bench(int gpu, int mapped, int workers, int device, size_t pool_c
             return -1;
         }
     }
-    uint64_t pushed, full;
-    double dur;
-    if (warmup > 0) producer(&pool, rings, workers, batch, packet_size, warmup, &pushed, &full, &dur);
+    bench_config_t bcfg = default_config();
+    bcfg.num_workers = workers;
+    bcfg.batch_size = batch;
+    bcfg.packet_size = packet_size;
+    if (warmup > 0) (void)run_producer(&bcfg, &pool, rings, warmup);
     uint64_t before[16];
     for (int i = 0; i < workers; i++) before[i] = __atomic_load_n(&ws[i].pkts_in, __ATOMIC_ACQUIRE);
-    producer(&pool, rings, workers, batch, packet_size, seconds, &pushed, &full, &dur);
+    const producer_result_t pr = run_producer(&bcfg, &pool, rings, seconds);
+    const uint64_t pushed = pr.packets_pushed, full = pr.ring_full_events;
+    const double dur = pr.duration_sec;
     uint64_t consumed = 0;
     for (int i = 0; i < workers; i++)
         consumed += __atomic_load_n(&ws[i].pkts_in, __ATOMIC_ACQUIRE) - before[i];
