@@ -402,9 +402,9 @@ typedef struct upe_worker_ops {
      * popped with the new state.  A nonzero return of sync() ends the loop with -1. */
     int (*poll)(void *user);
     int (*sync)(void *user, upe_gpu_ctx_t *ctx);
-    /* optional: after every GPU batch, the loop's counters so far (the worker_t fields the stats
-     * thread reads, src/main.c:284-315: pkts_in, pkts_parsed, pkts_matched, pkts_forwarded,
-     * pkts_dropped; the rest as upe_counters_t defines them) */
+    /* optional: after every GPU batch walked, and after every sync(), the loop's counters so far
+     * (the worker_t fields the stats thread reads, src/main.c:284-315: pkts_in, pkts_parsed,
+     * pkts_matched, pkts_forwarded, pkts_dropped; the rest as upe_counters_t defines them) */
     void (*publish)(void *user, upe_gpu_ctx_t *ctx, const upe_counters_t *counters);
 } upe_worker_ops_t;
 

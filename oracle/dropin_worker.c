@@ -76,6 +76,7 @@ typedef struct {
     const upe_worker_ops_t *ops;    /* NULL: g_ops */
     upe_worker_cfg_t cfg;
     const rule_table_t *rt_loaded;  /* the table the context holds */
+    rule_stat_t *stats_loaded;      /* the rule_stats array that goes with it */
     uint64_t stats_every_ns;        /* rule_stats published at most this often (0: every batch) */
     uint64_t stats_last_ns;
     upe_counters_t counters;        /* the loop's, at the end */
@@ -116,20 +117,26 @@ static int op_load_neigh(void *u, upe_gpu_ctx_t *ctx) {
 /* the stats thread swapped w->rt (and w->rule_stats) since the context's table was loaded */
 static int op_poll(void *u) { return GW(u)->w->rt != GW(u)->rt_loaded; }
 static int op_sync(void *u, upe_gpu_ctx_t *ctx) {
-    const rule_table_t *rt = GW(u)->w->rt;
+    /* the stats thread stored rule_stats before rt (src/main.c:261-263): with the new rt seen,
+     * the new rule_stats is the one to publish into from now on */
+    const rule_table_t *rt = __atomic_load_n(&GW(u)->w->rt, __ATOMIC_ACQUIRE);
     GW(u)->rt_loaded = rt;
+    GW(u)->stats_loaded = __atomic_load_n(&GW(u)->w->rule_stats, __ATOMIC_ACQUIRE);
     /* old rule_stats are not handed back: the stats thread frees the old array */
     return upe_gpu_reload_rules(ctx, (const upe_rule_t *)rt->rules, rt->count, rt->capacity, NULL, 0);
 }
 static void op_publish(void *u, upe_gpu_ctx_t *ctx, const upe_counters_t *c) {
     gpu_worker_t *g = GW(u);
     worker_t *w = g->w;
-    /* rule_stats into the array the stats thread reads — unless a swap is pending: the packets
-     * just classified ran with the old table, and w->rule_stats is already the new array */
+    /* rule_stats into the array the stats thread reads — unless a swap has begun: the packets
+     * just classified ran with the old table, and w->rule_stats may already be the new array
+     * (swapped before rt, src/main.c:261-263), so both pointers must still be the loaded ones */
     const uint64_t t = now_ns();
-    if (w->rt == g->rt_loaded && t - g->stats_last_ns >= g->stats_every_ns) {
+    rule_stat_t *rs = __atomic_load_n(&w->rule_stats, __ATOMIC_ACQUIRE);
+    if (rs == g->stats_loaded && __atomic_load_n(&w->rt, __ATOMIC_ACQUIRE) == g->rt_loaded &&
+        t - g->stats_last_ns >= g->stats_every_ns) {
         g->stats_last_ns = t;
-        (void)upe_gpu_get_stats(ctx, NULL, (upe_rule_stat_t *)w->rule_stats, w->rt->capacity);
+        (void)upe_gpu_get_stats(ctx, NULL, (upe_rule_stat_t *)rs, g->rt_loaded->capacity);
     }
     /* then the counters (release: a reader that sees them sees the rule_stats above) */
     __atomic_store_n(&w->pkts_in, c->pkts_in, __ATOMIC_RELEASE);
@@ -162,6 +169,7 @@ static void *gpu_worker_main(void *arg) {
         return NULL;
     }
     g->rt_loaded = w->rt;
+    g->stats_loaded = w->rule_stats;
     if (upe_gpu_load_rules(ctx, (const upe_rule_t *)w->rt->rules, w->rt->count) != 0 ||
         op_load_neigh(g, ctx) != 0 || upe_gpu_set_port(ctx, w->tx->eth_addr, w->tx->ip4_addr) != 0 ||
         upe_gpu_worker_run(ctx, g->ops ? g->ops : &g_ops, g, &g->cfg, &g->counters) != 0) {

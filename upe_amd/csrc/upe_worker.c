@@ -349,10 +349,15 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
         slot_t *G = &L.s[L.g];
         /* a change between bursts (polled after the pop: a burst pushed after the change was
          * made is classified with it): the packets held finish with the old state first */
-        if (ops->poll && ops->poll(user) && (finish_all(&L) != 0 || ops->sync(user, ctx) != 0)) {
-            G = &L.s[L.g];
-            for (unsigned r = 0; r < k; r++) G->bufs[G->n++] = burst[r];
-            goto fail;
+        if (ops->poll && ops->poll(user)) {
+            if (finish_all(&L) != 0 || ops->sync(user, ctx) != 0) {
+                G = &L.s[L.g];
+                for (unsigned r = 0; r < k; r++) G->bufs[G->n++] = burst[r];
+                goto fail;
+            }
+            /* the counters (and statistics) as they stand under the new state, even if no
+             * batch follows for a while */
+            if (ops->publish) ops->publish(user, ctx, &L.c);
         }
         if (k == 0) {
             if (G->n > 0 || L.o >= 0) { /* the ring is empty: classify what is held now */
