@@ -124,12 +124,6 @@ constexpr size_t kLdsDynMax = 136 * 1024;
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kRingMax = 64;           // batches of a ring launch whose completion is stamped
-#ifndef UPE_ABLATE
-#define UPE_ABLATE 0   // diagnostic builds only (make ablate); results are wrong when != 0
-#endif
-// 1 scan, 2 neighbour lookup, 4 stats/atomics, 8 stores, 16 general path, 64 empty classify,
-// 256 no fold of the previous batch into the L1 state
-constexpr unsigned kAblate = UPE_ABLATE;
 // Cache policy of the emit-mode record store: sc1 (buffer aux 16) writes the records through
 // and drops their lines from the XCD's L2, so the end of a launch has ~16 MB less dirty data to
 // write back at the kernel boundary (config B 24.5 -> 24.1 us per 1M batch; nt 24.5, sc0 sc1
@@ -1107,7 +1101,7 @@ __device__ __forceinline__ void general_path(Port a, uint8_t* p, uint32_t len, P
                     const uint32_t m = len_mask(len, j);
                     w[j] = (nw[j] & m) | (w[j] & ~m);
                 }
-                if (!(kAblate & 8)) {
+                {
                     uint4* q = reinterpret_cast<uint4*>(p);
                     store16(&q[0], make_uint4(w[0], w[1], w[2], w[3]));
                     store16(&q[1], make_uint4(w[4], w[5], w[6], w[7]));
@@ -1412,7 +1406,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
         return;
     }
-    if (kAblate & 64) return;
     STAMP(0);
     STAMP_WHERE();
     const int tid = threadIdx.x;
@@ -1575,13 +1568,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         }
     };
     auto fold_start = [&]() {
-        if (kAblate & 256) {   // diagnostic: no fold (wrong L1 state)
-#pragma unroll
-            for (int j = 0; j < 11; ++j) L1[j] = lin[j];
-        } else {
-            const L1Out o = reduce_l1r(pr);
-            fold_l1(lin, o.f4, o.f6, o.m4, o.m6, o.wg4, o.wg6, pay_prev(a), L1);
-        }
+        const L1Out o = reduce_l1r(pr);
+        fold_l1(lin, o.f4, o.f6, o.m4, o.m6, o.wg4, o.wg6, pay_prev(a), L1);
         look4 = L1[9] == 0u;    // the ARP entry disagrees with the table
         look6 = L1[10] == 0u;   // the NDP entry disagrees with the table
         folded = true;
@@ -1652,7 +1640,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint32_t e12 = w[3] & 0xFFFFu;          // bytes 12,13 (ethertype, byte-swapped)
         const bool fast4 = live && len >= 34u && e12 == 0x0008u && byte_of(w[3], 2) == 0x45u;
         const bool fast6 = live && len >= 54u && e12 == 0xDD86u;
-        const bool slow = live && !fast4 && !fast6 && !(kAblate & 16);
+        const bool slow = live && !fast4 && !fast6;
         Parsed r;
         // Tuple-space kernels (large tables): a wave holding any other frame parses all 64 on
         // the general path, which gives the fast path's results for the fast path's frames — one
@@ -1719,7 +1707,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // latency hides behind the scan (the answer is unused unless the packet is forwarded) ----
         uint32_t mlo = 0, mhi = 0;
         bool nhit = false;
-        if (ok && r.ttl > 1u && !(kAblate & 2)) {
+        if (ok && r.ttl > 1u) {
             if (!r.v6 && a.arp_lds)
                 nhit = arp_lookup_lds(s_arp, a.arp.bits, a.arp.seed, r.d[0], mlo, mhi);
             else if (r.v6 && a.ndp_lds)
@@ -1733,10 +1721,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint32_t k1 = r.dport;
         const bool need_v6 = __any(ok && r.v6);
         uint32_t ri, act = 0;   // act: the matched rule's x1 word (action code in bits 16-17)
-        if (kAblate & 1) {
-            ri = ok ? 0u : kNone;
-            act = 1u << 16;
-        } else if (kTssMode) {
+        if (kTssMode) {
             ri = tss_match_both(a, ok, r.v6, k0, k1, r.s, r.d, act, s_fps);
         } else {
             // small tables from their LDS copy, larger ones through the scalar unit
@@ -1901,7 +1886,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (hit) flags |= UPE_VF_NEIGH_HIT;
 
         // ---- write back ----
-        if (kEmit && live && code == UPE_V_FWD && !(kAblate & 8)) {
+        if (kEmit && live && code == UPE_V_FWD) {
             // record: bytes 0..11 as forwarded (neighbour + port MAC on a hit, else unchanged),
             // the new TTL / hop limit, the new IPv4 checksum, the family
             uint4 rec;
@@ -1916,7 +1901,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 __builtin_amdgcn_raw_buffer_store_b128(v4u{rec.x, rec.y, rec.z, rec.w}, rs,
                                                        rslot * 16u, 0, kRecAux);
             }
-        } else if (!kEmit && live && !(kAblate & 8)) {
+        } else if (!kEmit && live) {
             uint4* q = reinterpret_cast<uint4*>(a.frames + ((size_t)off16 << 4));
             if (hit)
                 store16(&q[0], make_uint4(mlo, mhi | (a.port_mac_lo << 16),
@@ -1953,7 +1938,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         // cheaper than a cross-lane reduction per distinct rule).  One 64-bit atomic per packet:
         // the bin's low word counts packets, the high word bytes; neither carries into the other
         // (a workgroup's packets and bytes each fit 32 bits, as the u32 views below assume) ----
-        if (lds_stats && !(kAblate & 4) && ok && ri != kNone)
+        if (lds_stats && ok && ri != kNone)
             atomicAdd(reinterpret_cast<unsigned long long*>(&lds_hist[2 * rsi]),
                       ((unsigned long long)len << 32) | 1ull);
 
@@ -2053,7 +2038,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // totals (the host sums them and credits rule_id; nothing in this launch reads them), so
     // that the hot rules' counters take 1/kStatReps of the workgroups' atomics each (by every
     // wave but the counting one) ----
-    if (lds_stats && !small_stats && !(kAblate & 4) && !(counting && kWaves > 1 && wave == kCounter)) {
+    if (lds_stats && !small_stats && !(counting && kWaves > 1 && wave == kCounter)) {
         unsigned long long* rep = a.stats_idx + (size_t)(blockIdx.x % kStatReps) * 2 * a.nrules_pad;
         const uint32_t skip = counting && kWaves > 1 ? 64u : 0u;
         const uint32_t t0 = (uint32_t)tid - (counting && kWaves > 1 && wave > kCounter ? 64u : 0u);
@@ -2077,7 +2062,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     const uint32_t m6 = wave_reduce<2>(lane < kWaves ? s_wm[lane][1] << 4 | (uint32_t)lane : 0u);
     const uint32_t x4 = m4 >> 4, x6 = m6 >> 4;
     const int w4 = (int)(m4 & 15u), w6 = (int)(m6 & 15u);
-    if (!(kAblate & 4)) {
+    {
         const uint32_t cv = lane < C_N ? s_tot[lane] : 0u;   // lane c < C_N: counter c
         if (lane < C_N && cv) atomicAdd(&acc_cur(a)->cnt[rep][lane], cv);
         // the L1 outcome, one atomicMax instruction: minima as kNone - x, the last table hits
@@ -4169,7 +4154,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     const bool lds_stats = c->nrules_pad <= (uint32_t)kLdsStatsMax;
     a.gb = nullptr;
     a.gb_packed = c->nrules <= 65536u ? 1u : 0u;   // sorted indexes of matches < nrules
-    if (!lds_stats && n > 0 && !(kAblate & 4)) {
+    if (!lds_stats && n > 0) {
         if (n > c->gb_alloc) {
             if (c->gb) (void)hipFree(c->gb);
             c->gb = nullptr;
@@ -4285,7 +4270,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     HIP_TRY(hipGetLastError());
     c->last_var = var;
     c->last_grid = grid;
-    const bool group_by = !lds_stats && n > 0 && !(kAblate & 4);
+    const bool group_by = !lds_stats && n > 0;
     // the sample's middle event, between the classify launch and the group-by (last call of the
     // sample only; launches without a group-by have none)
     const bool mid = c->t_left == 1 && group_by;
