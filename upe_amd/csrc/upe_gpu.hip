@@ -296,12 +296,13 @@ constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 //   node (uint2): inner {dim | child << 5, threshold}: key word < threshold -> child, else child+1
 //                 leaf  {16 | count << 5, first entry}
 //   leaf entry (u32): list position | 0x80000000 when the rule matches every key of the leaf
-// Each family's rules are split into groups by the key word on which each is narrowest, one
+// Each family's rules are split into groups by the key field on which each is narrowest, one
 // tree per group (a rule narrow only in a port is then not copied into every leaf of a tree cut on
-// addresses); a key's first match is the smallest of its first matches over its family's trees.
-// Image: a directory (node 0 = {IPv4 trees, IPv6 trees}, then a copy of each tree's root, IPv4
-// first), the nodes, then the leaf entries; staged in LDS when it fits beside the launch's other
-// LDS data.
+// addresses); a key's first match is the smallest of its first matches over its family's trees,
+// else the family's rule that matches every key (build_forest_family).
+// Image: a directory (node 0 = {IPv4 trees, IPv6 trees}, node 1 = {IPv4, IPv6 default answer},
+// then a copy of each tree's root, IPv4 first), the nodes, then the leaf entries; staged in LDS
+// when it fits beside the launch's other LDS data.
 constexpr int kTreeDims = 11;
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
 
@@ -808,7 +809,7 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
     const uint2 dir = N[0];
     const uint32_t ntw = __builtin_amdgcn_readfirstlane(dir.x > dir.y ? dir.x : dir.y);
-    const uint32_t nt = active ? (is6 ? dir.y : dir.x) : 0u, first = 1u + (is6 ? dir.x : 0u);
+    const uint32_t nt = active ? (is6 ? dir.y : dir.x) : 0u, first = 2u + (is6 ? dir.x : 0u);
     // key word `dim`: address words raw (IPv6 byte-swapped below), ports and protocol from k0/k1
     const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
@@ -869,6 +870,15 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                     }
                 }
             }
+        }
+    }
+    if (__any(active && best == kNone)) {
+        // no tree's rule: the family's rule that matches every key, if it has one
+        const uint2 dflt = N[1];
+        const uint32_t d = is6 ? dflt.y : dflt.x;
+        if (active && best == kNone && d != kNone) {
+            best = d;
+            bact = (is6 ? g6[(size_t)kFamV6Stride * d] : a.fam[2 * (size_t)d]).z;
         }
     }
     act = bact;
@@ -3359,20 +3369,31 @@ bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_
     return true;
 }
 
-// One family's forest: its rules grouped by the key word on which each overlaps the fewest
-// other rules of the list (EffiCuts-style separation: a rule narrow only in its destination port
-// is not copied into every leaf of a tree that splits on addresses), one tree per group, every
-// tree's rules in list order.  A key's first match is the smallest of its first matches in the
-// trees (the groups partition the list).  A rule that matches every key of the family (the list's
-// last entry, if any) gets a one-leaf tree of its own.
+// One family's forest: its rules grouped by the key field (source address, destination address,
+// source port, destination port, protocol) whose word overlaps the fewest other rules of the list
+// (EffiCuts-style separation: a rule narrow only in its destination port is not copied into every
+// leaf of a tree that splits on addresses; an address prefix is exact on its leading words, so
+// one tree per address field splits on any of its words without copies), one tree per group,
+// every tree's rules in list order; groups of fewer than kTreeMinGroup rules share one tree.  A
+// key's first match is the smallest of its first matches in the trees (the groups partition the
+// list).  The family's rule that matches every key (the list's last entry, if any) is no tree's:
+// it is the answer when no tree has one (*def, its list position, else kNone).
+constexpr int kTreeFields = 5;
+constexpr size_t kTreeMinGroup = 8;
+int tree_field(int d) { return d < 4 ? 0 : d < 8 ? 1 : d - 6; }
 bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
-                         size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots) {
+                         size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots,
+                         uint32_t* def) {
     const size_t n = R.size();
     roots.clear();
+    *def = kNone;
     if (n == 0) return true;
     std::vector<int> grp(n, -1);
     std::vector<uint32_t> best(n, 0xFFFFFFFFu);
     std::vector<uint32_t> los(n), his(n);
+    const char* gm = getenv("UPE_GPU_TREE_GROUP");   // diagnostic: "word" = one group per key word
+    const bool by_word = gm && gm[0] == 'w';
+    const int ng = by_word ? kTreeDims : kTreeFields;
     for (int d = 0; d < kTreeDims; ++d) {
         for (size_t i = 0; i < n; ++i) {
             los[i] = R[i].lo[d];
@@ -3387,7 +3408,7 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
             const uint32_t ov = (uint32_t)(a - b);
             if (ov < best[i]) {
                 best[i] = ov;
-                grp[i] = d;
+                grp[i] = by_word ? d : tree_field(d);
             }
         }
     }
@@ -3395,12 +3416,22 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
         bool all = true;
         for (int d = 0; d < kTreeDims && all; ++d)
             all = (R[i].exact >> d & 1u) && R[i].lo[d] == 0 && R[i].hi[d] == kTreeWidth[d];
-        if (all) grp[i] = kTreeDims;   // matches every key of the family
+        if (all) {   // matches every key of the family (the list ends with it)
+            grp[i] = -1;
+            if (*def == kNone) *def = (uint32_t)i;
+        }
     }
-    for (int g = 0; g <= kTreeDims; ++g) {
-        std::vector<uint32_t> members;
-        for (size_t i = 0; i < n; ++i)
-            if (grp[i] == g) members.push_back((uint32_t)i);
+    std::vector<std::vector<uint32_t>> groups(ng + 1);
+    for (size_t i = 0; i < n; ++i)
+        if (grp[i] >= 0) groups[grp[i]].push_back((uint32_t)i);
+    for (int g = 0; g < ng; ++g)   // small groups share one tree (kept in list order)
+        if (!groups[g].empty() && groups[g].size() < kTreeMinGroup) {
+            groups[ng].insert(groups[ng].end(), groups[g].begin(), groups[g].end());
+            groups[g].clear();
+        }
+    std::sort(groups[ng].begin(), groups[ng].end());
+    for (int g = 0; g <= ng; ++g) {
+        const std::vector<uint32_t>& members = groups[g];
         if (members.empty()) continue;
         roots.push_back((uint32_t)img.nodes.size());
         const size_t n0 = img.nodes.size(), e0 = img.leaves.size();
@@ -3417,8 +3448,9 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
 }
 
 // The forests of both family lists (l4 / l6: sorted indexes of the list entries), after a
-// directory: node 0 = {trees of family 4, trees of family 6}, then a copy of each tree's root
-// (family 4's trees first), so that a walk starts without an indirection.
+// directory: node 0 = {trees of family 4, trees of family 6}, node 1 = the families' default
+// answers (list positions, kNone = none), then a copy of each tree's root (family 4's trees
+// first), so that a walk starts without an indirection.
 bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
                 const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, uint32_t binth,
                 size_t node_budget, TreeImage& img) {
@@ -3426,16 +3458,18 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     TreeImage body;
     std::vector<TreeRule> R;
     std::vector<uint32_t> r4, r6;
+    uint32_t def4 = kNone, def6 = kNone;
     for (uint32_t i : l4) R.push_back(tree_rule(4, v4[i], nullptr));
-    if (!build_forest_family(R, 0, binth, node_budget, body, r4)) return false;
+    if (!build_forest_family(R, 0, binth, node_budget, body, r4, &def4)) return false;
     R.clear();
     for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i]));
-    if (!build_forest_family(R, 1, binth, node_budget, body, r6)) return false;
-    const uint32_t dir = 1u + (uint32_t)(r4.size() + r6.size());
+    if (!build_forest_family(R, 1, binth, node_budget, body, r6, &def6)) return false;
+    const uint32_t dir = 2u + (uint32_t)(r4.size() + r6.size());
     auto shift = [&](uint2 nd) {   // inner nodes' child indexes move by the directory's size
         return (nd.x & 16u) ? nd : make_uint2((nd.x & 15u) | (((nd.x >> 5) + dir) << 5), nd.y);
     };
     img.nodes.push_back(make_uint2((uint32_t)r4.size(), (uint32_t)r6.size()));
+    img.nodes.push_back(make_uint2(def4, def6));
     for (uint32_t r : r4) img.nodes.push_back(shift(body.nodes[r]));
     for (uint32_t r : r6) img.nodes.push_back(shift(body.nodes[r]));
     for (uint2 nd : body.nodes) img.nodes.push_back(shift(nd));
@@ -3454,8 +3488,8 @@ uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
                         const std::vector<RuleV6>& v6, const std::vector<uint32_t>& list, bool is6,
                         const uint32_t kv[kTreeDims], uint32_t k0, uint32_t k1, const uint32_t s[4],
                         const uint32_t d[4]) {
-    const uint2 dir = img.nodes[0];
-    const uint32_t nt = is6 ? dir.y : dir.x, first = 1u + (is6 ? dir.x : 0u);
+    const uint2 dir = img.nodes[0], dflt = img.nodes[1];
+    const uint32_t nt = is6 ? dir.y : dir.x, first = 2u + (is6 ? dir.x : 0u);
     uint32_t best = kNone;
     for (uint32_t t = 0; t < nt; ++t) {
         uint2 nd = img.nodes[first + t];
@@ -3483,7 +3517,7 @@ uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
             }
         }
     }
-    return best;
+    return best != kNone ? best : is6 ? dflt.y : dflt.x;
 }
 
 // rule_t -> the compiled words: RuleV4 / RuleV6 (pre-masked) and rinfo, pad >= count entries (the
