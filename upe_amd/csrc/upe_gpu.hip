@@ -304,6 +304,11 @@ constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 // then a copy of each tree's root, IPv4 first), the nodes, then the leaf entries; staged in LDS
 // when it fits beside the launch's other LDS data.
 constexpr int kTreeDims = 11;
+#ifndef UPE_TREE_ILP
+#define UPE_TREE_ILP 3
+#endif
+constexpr int kTreeIlp = UPE_TREE_ILP;   // trees a lane walks at once (tree_match)
+static_assert(kTreeIlp >= 1 && kTreeIlp <= 3, "tree_match spells out up to three walks");
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
 
 struct Args {
@@ -814,13 +819,22 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
-    for (uint32_t t = 0; t < ntw; ++t) {
-        uint2 nd = make_uint2(16u, 0u);   // lanes without a tree t: an empty leaf
-        if (t < nt) nd = N[first + t];
-        while (__any(!(nd.x & 16u))) {
-            if (!(nd.x & 16u)) {
+    for (uint32_t t0 = 0; t0 < ntw; t0 += kTreeIlp) {
+        // kTreeIlp trees walked together: one node load per tree and level, all in flight at once
+        // (a lane whose walk of a tree has ended reloads the directory word, a broadcast)
+        uint2 nds[kTreeIlp];
+#pragma unroll
+        for (int u = 0; u < kTreeIlp; ++u)   // lanes without a tree t0 + u: an empty leaf
+            nds[u] = t0 + u < nt ? N[first + t0 + u] : make_uint2(16u, 0u);
+        for (;;) {
+            bool more = false;
+#pragma unroll
+            for (int u = 0; u < kTreeIlp; ++u) more = more || !(nds[u].x & 16u);
+            if (!__any(more)) break;
+            auto advance = [&](uint2& ndr) {
                 // (bit selects, so that the key words stay in registers: a select between
                 // elements of s / d becomes an indexed load of a scratch copy otherwise)
+                const uint2 nd = ndr;
                 const uint32_t dim = nd.x & 15u;
                 const uint32_t m1 = 0u - (dim & 1u), m2 = 0u - ((dim >> 1) & 1u);
                 const uint32_t m4 = 0u - ((dim >> 2) & 1u), m8 = 0u - ((dim >> 3) & 1u);
@@ -829,9 +843,20 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                 uint32_t v = vsel(m4, da, sa);
                 if (is6) v = bswap32(v);
                 v = vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), v);
-                nd = N[(nd.x >> 5) + (v >= nd.y ? 1u : 0u)];
-            }
+                const bool leaf = (nd.x & 16u) != 0u;
+                const uint2 nx = N[leaf ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u)];
+                ndr = leaf ? nd : nx;
+            };
+            // (spelled out: the compiler would not unroll a loop over the trees here)
+            advance(nds[0]);
+            if constexpr (kTreeIlp > 1) advance(nds[1]);
+            if constexpr (kTreeIlp > 2) advance(nds[2]);
         }
+        for (int u = 0; u < kTreeIlp; ++u) {   // the leaves, tree by tree
+        uint2 nd = nds[0];
+#pragma unroll
+        for (int q = 1; q < kTreeIlp; ++q)   // (selects: nds stays in registers)
+            if (u == q) nd = nds[q];
         const uint32_t cnt = nd.x >> 5;
         bool look = cnt != 0u;
         for (uint32_t j = 0; __any(look); ++j) {
@@ -871,14 +896,15 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                 }
             }
         }
+        }
     }
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
         const uint2 dflt = N[1];
-        const uint32_t d = is6 ? dflt.y : dflt.x;
-        if (active && best == kNone && d != kNone) {
-            best = d;
-            bact = (is6 ? g6[(size_t)kFamV6Stride * d] : a.fam[2 * (size_t)d]).z;
+        const uint32_t dv = is6 ? dflt.y : dflt.x;
+        if (active && best == kNone && dv != kNone) {
+            best = dv;
+            bact = (is6 ? g6[(size_t)kFamV6Stride * dv] : a.fam[2 * (size_t)dv]).z;
         }
     }
     act = bact;
