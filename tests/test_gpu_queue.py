@@ -33,8 +33,12 @@ def _run(w, wl, bounds, queue: bool):
         for p in parts:
             w.process_emit(*p)
     frames, verdict = b.fetch()
-    rec = b.fetch_hdr()
+    raw = b.fetch_hdr(raw=True)
     b.free()
+    # each batch's records are compacted per 64-packet group counted from its own first packet
+    rec = np.zeros_like(raw)
+    for s, e in zip(bounds[:-1], bounds[1:]):
+        rec[s:e] = gpu.expand_records(raw[s:e], verdict[s:e])
     return frames, verdict, rec
 
 
