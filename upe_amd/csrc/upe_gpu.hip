@@ -40,8 +40,9 @@
 // Neighbour lookups answer arp_get_mac / ndp_get_mac exactly without walking the reference's
 // linear-probe chains: at upload the host keeps only the entries a reference probe can reach
 // (probe from the home slot, first valid match before the first invalid slot) and places them
-// by two-choice cuckoo hashing; every answer equals the reference's for the snapshot and a
-// lookup is one LDS read (indexes of up to 2048 slots are staged) or one memory round trip.
+// by three-choice cuckoo hashing; every answer equals the reference's for the snapshot and a
+// lookup is three independent LDS reads (indexes of up to 2048 slots are staged) or one memory
+// round trip.
 //
 // The worker's one-entry L1 neighbour caches are sequential state (src/worker.c:186-195,
 // 218-225), emulated exactly.  If the starting L1 entry agrees with the
@@ -239,7 +240,7 @@ struct DevState {
 };
 
 // Neighbour index (built by upe_gpu_load_neigh): the entries a reference probe reaches, placed
-// by two-choice cuckoo hashing, so that every key sits in one of its two candidate slots.
+// by three-choice cuckoo hashing, so that every key sits in one of its three candidate slots.
 //   ARP slot: uint4 {ip, mac0..3, mac4..5 | used << 16, 0}
 //   NDP slot: 2 x uint4 {ip words 0..3}, {mac0..3, mac4..5 | used << 16, 0, 0}
 struct NeighIndex {
@@ -324,6 +325,7 @@ struct Args {
     const uint4* fam;
     uint32_t fam4, fam6;           // entries per list, multiples of kUnroll
     uint32_t fam6_lds;             // the IPv6 list is staged in LDS (after the neighbour indexes)
+    uint32_t fam4_lds;             // (tree kernels) the IPv4 list too, after the IPv6 one
     uint32_t fam_x1idx;            // tables below 8192 rules: each entry's x1 bits 18-30 carry its
                                    // sorted index (no index-array load after a match)
     // decision-tree index over the family lists (kTreeDims comment)
@@ -489,56 +491,61 @@ __host__ __device__ __forceinline__ uint32_t slot2(uint32_t k, uint32_t seed, ui
     const uint32_t x = (k ^ seed) * 0x85EBCA77u;
     return ((x ^ (x >> 16)) * 0xC2B2AE3Du) >> (32 - bits);
 }
+// The neighbour indexes' third choice (round 5: three-choice cuckoo placement fills the slots to
+// ~0.6-0.8 instead of two-choice's < 0.5, so an index takes half the LDS: config C's ARP and NDP
+// indexes 96 -> 48 KB, config B's ARP index 16 -> 8 KB)
+__host__ __device__ __forceinline__ uint32_t slot3(uint32_t k, uint32_t seed, uint32_t bits) {
+    const uint32_t x = (k ^ (seed * 0x9E3779B9u)) * 0x27D4EB2Fu;
+    return ((x ^ (x >> 15)) * 0x165667B1u) >> (32 - bits);
+}
+__device__ __forceinline__ bool arp_slot_hit(const uint4& e, uint32_t ip) {
+    return ((e.z >> 16) & 1u) && e.x == ip;
+}
 __device__ __forceinline__ bool arp_lookup(const NeighIndex& x, uint32_t ip, uint32_t& lo,
                                            uint32_t& hi) {
     if (x.bits == 0) return false;
     const uint4 e1 = x.t[slot1(ip, x.seed, x.bits)];
     const uint4 e2 = x.t[slot2(ip, x.seed, x.bits)];
-    const bool h1 = ((e1.z >> 16) & 1u) && e1.x == ip;
-    const bool h2 = ((e2.z >> 16) & 1u) && e2.x == ip;
-    lo = h1 ? e1.y : e2.y;
-    hi = (h1 ? e1.z : e2.z) & 0xFFFFu;
-    return h1 || h2;
+    const uint4 e3 = x.t[slot3(ip, x.seed, x.bits)];
+    const bool h1 = arp_slot_hit(e1, ip), h2 = arp_slot_hit(e2, ip), h3 = arp_slot_hit(e3, ip);
+    const uint4 e = h1 ? e1 : h2 ? e2 : e3;
+    lo = e.y;
+    hi = e.z & 0xFFFFu;
+    return h1 || h2 || h3;
 }
 // The same lookup against an LDS copy of the slot array.
 __device__ __forceinline__ bool arp_lookup_lds(const uint4* t, uint32_t bits, uint32_t seed,
                                                uint32_t ip, uint32_t& lo, uint32_t& hi) {
     const uint4 e1 = t[slot1(ip, seed, bits)];
     const uint4 e2 = t[slot2(ip, seed, bits)];
-    const bool h1 = ((e1.z >> 16) & 1u) && e1.x == ip;
-    const bool h2 = ((e2.z >> 16) & 1u) && e2.x == ip;
-    lo = h1 ? e1.y : e2.y;
-    hi = (h1 ? e1.z : e2.z) & 0xFFFFu;
-    return h1 || h2;
+    const uint4 e3 = t[slot3(ip, seed, bits)];
+    const bool h1 = arp_slot_hit(e1, ip), h2 = arp_slot_hit(e2, ip), h3 = arp_slot_hit(e3, ip);
+    const uint4 e = h1 ? e1 : h2 ? e2 : e3;
+    lo = e.y;
+    hi = e.z & 0xFFFFu;
+    return h1 || h2 || h3;
+}
+__device__ __forceinline__ bool ndp_slot_hit(const uint4& a, const uint4& m, const uint32_t ip[4]) {
+    return ((m.y >> 16) & 1u) && a.x == ip[0] && a.y == ip[1] && a.z == ip[2] && a.w == ip[3];
 }
 __device__ __forceinline__ bool ndp_lookup_lds(const uint4* t, uint32_t bits, uint32_t seed,
                                                const uint32_t ip[4], uint32_t& lo, uint32_t& hi) {
     const uint32_t k = fold_v6(ip);
-    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits);
+    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits), t3 = slot3(k, seed, bits);
     const uint4 a1 = t[2 * t1], m1 = t[2 * t1 + 1];
     const uint4 a2 = t[2 * t2], m2 = t[2 * t2 + 1];
-    const bool h1 = ((m1.y >> 16) & 1u) && a1.x == ip[0] && a1.y == ip[1] && a1.z == ip[2] &&
-                    a1.w == ip[3];
-    const bool h2 = ((m2.y >> 16) & 1u) && a2.x == ip[0] && a2.y == ip[1] && a2.z == ip[2] &&
-                    a2.w == ip[3];
-    lo = h1 ? m1.x : m2.x;
-    hi = (h1 ? m1.y : m2.y) & 0xFFFFu;
-    return h1 || h2;
+    const uint4 a3 = t[2 * t3], m3 = t[2 * t3 + 1];
+    const bool h1 = ndp_slot_hit(a1, m1, ip), h2 = ndp_slot_hit(a2, m2, ip),
+               h3 = ndp_slot_hit(a3, m3, ip);
+    const uint4 m = h1 ? m1 : h2 ? m2 : m3;
+    lo = m.x;
+    hi = m.y & 0xFFFFu;
+    return h1 || h2 || h3;
 }
 __device__ __forceinline__ bool ndp_lookup(const NeighIndex& x, const uint32_t ip[4], uint32_t& lo,
                                            uint32_t& hi) {
     if (x.bits == 0) return false;
-    const uint32_t k = fold_v6(ip);
-    const uint32_t t1 = slot1(k, x.seed, x.bits), t2 = slot2(k, x.seed, x.bits);
-    const uint4 a1 = x.t[2 * t1], m1 = x.t[2 * t1 + 1];
-    const uint4 a2 = x.t[2 * t2], m2 = x.t[2 * t2 + 1];
-    const bool h1 = ((m1.y >> 16) & 1u) && a1.x == ip[0] && a1.y == ip[1] && a1.z == ip[2] &&
-                    a1.w == ip[3];
-    const bool h2 = ((m2.y >> 16) & 1u) && a2.x == ip[0] && a2.y == ip[1] && a2.z == ip[2] &&
-                    a2.w == ip[3];
-    lo = h1 ? m1.x : m2.x;
-    hi = (h1 ? m1.y : m2.y) & 0xFFFFu;
-    return h1 || h2;
+    return ndp_lookup_lds(x.t, x.bits, x.seed, ip, lo, hi);
 }
 
 // Both families in one lookup: the IPv4 (ARP) and IPv6 (NDP) lanes of a wave issue their slot
@@ -551,23 +558,22 @@ __device__ __forceinline__ bool neigh_lookup(const NeighIndex& arp, const NeighI
     const uint32_t seed = v6 ? ndp.seed : arp.seed;
     if (bits == 0) return false;
     const uint32_t k = v6 ? fold_v6(d) : d[0];
-    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits);
+    const uint32_t t1 = slot1(k, seed, bits), t2 = slot2(k, seed, bits), t3 = slot3(k, seed, bits);
     const uint32_t sh = v6 ? 1u : 0u;   // an NDP slot is two uint4: address, then MAC
-    const uint4 a1 = t[t1 << sh], a2 = t[t2 << sh];
-    uint4 m1 = a1, m2 = a2;
+    const uint4 a1 = t[t1 << sh], a2 = t[t2 << sh], a3 = t[t3 << sh];
+    uint4 m1 = a1, m2 = a2, m3 = a3;
     if (v6) {
         m1 = t[2 * t1 + 1];
         m2 = t[2 * t2 + 1];
+        m3 = t[2 * t3 + 1];
     }
-    const bool h1 = v6 ? (((m1.y >> 16) & 1u) && a1.x == d[0] && a1.y == d[1] && a1.z == d[2] &&
-                          a1.w == d[3])
-                       : (((a1.z >> 16) & 1u) && a1.x == d[0]);
-    const bool h2 = v6 ? (((m2.y >> 16) & 1u) && a2.x == d[0] && a2.y == d[1] && a2.z == d[2] &&
-                          a2.w == d[3])
-                       : (((a2.z >> 16) & 1u) && a2.x == d[0]);
-    lo = h1 ? (v6 ? m1.x : a1.y) : (v6 ? m2.x : a2.y);
-    hi = (h1 ? (v6 ? m1.y : a1.z) : (v6 ? m2.y : a2.z)) & 0xFFFFu;
-    return h1 || h2;
+    const bool h1 = v6 ? ndp_slot_hit(a1, m1, d) : arp_slot_hit(a1, d[0]);
+    const bool h2 = v6 ? ndp_slot_hit(a2, m2, d) : arp_slot_hit(a2, d[0]);
+    const bool h3 = v6 ? ndp_slot_hit(a3, m3, d) : arp_slot_hit(a3, d[0]);
+    const uint4 e = h1 ? (v6 ? m1 : a1) : h2 ? (v6 ? m2 : a2) : (v6 ? m3 : a3);
+    lo = v6 ? e.x : e.y;
+    hi = (v6 ? e.y : e.z) & 0xFFFFu;
+    return h1 || h2 || h3;
 }
 
 // Does each L1 entry agree with the table?  (ARP: an entry for 0.0.0.0 is never consulted,
@@ -809,7 +815,8 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
 template <bool kLdsTree>
 __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4], const uint32_t d[4],
-                                               uint32_t& act, const uint2* lnodes, const uint4* l6) {
+                                               uint32_t& act, const uint2* lnodes, const uint4* l6,
+                                               const uint4* l4) {
     const uint2* N = kLdsTree ? lnodes : a.tree;
     const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
     const uint2 dir = N[0];
@@ -876,6 +883,10 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                         const uint4* f = g6 + (size_t)kFamV6Stride * p;
                         e0 = f[0];
                         if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                    } else if (a.fam4_lds) {
+                        const uint4* f = l4 + 2 * p;
+                        e0 = f[0];
+                        if (!cov) e1 = f[1];
                     } else {
                         const uint4* f = a.fam + 2 * (size_t)p;
                         e0 = f[0];
@@ -1560,6 +1571,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         const uint4* g = a.fam + 2 * (size_t)a.fam4;
         for (uint32_t k = tid; k < kFamV6Stride * a.fam6; k += kBlock) s_fam6[k] = g[k];
     }
+    // (tree kernels) the IPv4 list as well, for the leaves' rule tests
+    uint4* s_fam4 = s_fam6 + (a.fam6_lds ? kFamV6Stride * a.fam6 : 0u);
+    if (kTree && a.fam4_lds)
+        for (uint32_t k = tid; k < 2 * a.fam4; k += kBlock) s_fam4[k] = a.fam[k];
     const uint16_t* s_fps = kTssMode && a.fp_lds ? reinterpret_cast<const uint16_t*>(s_fp4) : nullptr;
     __syncthreads();
     STAMP(1);
@@ -1764,8 +1779,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const uint32_t nr = a.nrules_pad;
             if (kTree)
                 ri = a.tree_lds ? tree_match<true>(a, ok, r.v6, k0, k1, r.s, r.d, act,
-                                                   reinterpret_cast<const uint2*>(s_tree), s_fam6)
-                                : tree_match<false>(a, ok, r.v6, k0, k1, r.s, r.d, act, nullptr, s_fam6);
+                                                   reinterpret_cast<const uint2*>(s_tree), s_fam6,
+                                                   s_fam4)
+                                : tree_match<false>(a, ok, r.v6, k0, k1, r.s, r.d, act, nullptr,
+                                                    s_fam6, s_fam4);
             else if (kFam)
                 ri = need_v6 ? scan_fam<true>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6)
                              : scan_fam<false>(a, !ok, r.v6, k0, k1, r.s, r.d, act, s_fam6);
@@ -2599,10 +2616,56 @@ template <class H>
 int cuckoo_place_fn(size_t n, H hfn, uint32_t& bits, uint32_t& seed, std::vector<int32_t>& slot,
                     uint32_t ratio_x2 = 5);
 
-int cuckoo_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& seed,
-                 std::vector<int32_t>& slot) {
-    return cuckoo_place_fn(key.size(), [&](size_t j, uint32_t) { return key[j]; }, bits, seed,
-                           slot);
+// Three-choice cuckoo placement of the neighbour indexes' keys (slot1 / slot2 / slot3): starts at
+// 2^bits >= 1.25 n slots, random-walk eviction, seeds tried, then doubles.  bits = 0 for no keys.
+int cuckoo3_place(const std::vector<uint32_t>& key, uint32_t& bits, uint32_t& seed,
+                  std::vector<int32_t>& slot) {
+    const size_t n = key.size();
+    slot.clear();
+    bits = 0;
+    seed = 0;
+    if (n == 0) return 0;
+    bits = 1;
+    while (((size_t)1 << bits) * 4 < n * 5) ++bits;
+    for (; bits <= 31; ++bits) {
+        const size_t m = (size_t)1 << bits;
+        for (uint32_t attempt = 0; attempt < 64; ++attempt) {
+            const uint32_t sd = attempt * 0x6D2B79F5u + bits;
+            slot.assign(m, -1);
+            uint32_t rnd = sd | 1u;
+            bool ok = true;
+            for (size_t j = 0; j < n && ok; ++j) {
+                int32_t cur = (int32_t)j;
+                uint32_t from = ~0u;
+                for (int kick = 0;; ++kick) {
+                    const uint32_t c[3] = {slot1(key[cur], sd, bits), slot2(key[cur], sd, bits),
+                                           slot3(key[cur], sd, bits)};
+                    int placed = -1;
+                    for (int q = 0; q < 3 && placed < 0; ++q)
+                        if (slot[c[q]] < 0) placed = q;
+                    if (placed >= 0) {
+                        slot[c[placed]] = cur;
+                        break;
+                    }
+                    if (kick >= 1000) {
+                        ok = false;
+                        break;
+                    }
+                    // evict a random choice other than the slot the key was just evicted from
+                    rnd ^= rnd << 13; rnd ^= rnd >> 17; rnd ^= rnd << 5;
+                    uint32_t q = rnd % 3u;
+                    if (c[q] == from) q = (q + 1) % 3u;
+                    std::swap(cur, slot[c[q]]);
+                    from = c[q];
+                }
+            }
+            if (ok) {
+                seed = sd;
+                return 0;
+            }
+        }
+    }
+    return -1;
 }
 
 // Same, with a seed-dependent 32-bit hash per key: hfn(j, seed).
@@ -4019,7 +4082,7 @@ int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_
             }
         }
     }
-    // Place the reachable entries by two-choice cuckoo hashing at load factor <= 0.4.
+    // Place the reachable entries by three-choice cuckoo hashing at load factor <= 0.8.
     std::vector<uint32_t> akey(arp_keep.size()), nkey(ndp_keep.size());
     for (size_t j = 0; j < arp_keep.size(); ++j) akey[j] = arp[arp_keep[j]].ip;
     std::vector<std::array<uint32_t, 4>> nwords(ndp_keep.size());
@@ -4030,7 +4093,7 @@ int upe_gpu_load_neigh(upe_gpu_ctx_t* c, const upe_arp_entry_t* arp, size_t arp_
     }
     uint32_t abits = 0, aseed = 0, nbits = 0, nseed = 0;
     std::vector<int32_t> aslot, nslot;   // slot -> entry (index into *_keep), -1 empty
-    if (cuckoo_place(akey, abits, aseed, aslot) != 0 || cuckoo_place(nkey, nbits, nseed, nslot) != 0)
+    if (cuckoo3_place(akey, abits, aseed, aslot) != 0 || cuckoo3_place(nkey, nbits, nseed, nslot) != 0)
         return fail("neighbour index: cuckoo placement failed");
     std::vector<uint4> a(aslot.size(), make_uint4(0, 0, 0, 0));
     for (size_t t = 0; t < aslot.size(); ++t) {
@@ -4261,6 +4324,12 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
         a.fam6_lds = 1u;
         lds += kFamV6Stride * c->fam6 * sizeof(uint4);
+    }
+    // the tree kernels' leaf tests read the IPv4 list's rule words too: from LDS when it fits
+    a.fam4_lds = 0u;
+    if (scan == 3 && c->tree_stage && c->fam4 && lds + 2 * c->fam4 * sizeof(uint4) <= kLdsDynMax) {
+        a.fam4_lds = 1u;
+        lds += 2 * c->fam4 * sizeof(uint4);
     }
     // the lean emit kernel when nothing it leaves out is needed (non-empty neighbour indexes
     // all in LDS, no flow_hash, no length side array)
