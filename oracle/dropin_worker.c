@@ -23,6 +23,8 @@
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
+#include <execinfo.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <sched.h>
 #include <signal.h>
@@ -204,26 +206,28 @@ static unsigned op_pop_logged(void *u, void **b, unsigned m) {
     return k;
 }
 
-static size_t index_of(pktbuf_t *const *all, size_t n, const pktbuf_t *b) {
-    /* `all` holds the run's buffers in packet order; they are distinct pool slots */
-    static const pktbuf_t *const *s_all;
-    static size_t s_n, *s_idx, s_lo, s_span;
-    if (s_all != (const pktbuf_t *const *)all || s_n != n) {
-        s_all = (const pktbuf_t *const *)all;
-        s_n = n;
-        size_t lo = (size_t)-1, hi = 0;
-        for (size_t i = 0; i < n; i++) {
-            size_t a = (size_t)all[i];
-            lo = a < lo ? a : lo;
-            hi = a > hi ? a : hi;
-        }
-        s_lo = lo;
-        s_span = (hi - lo) / sizeof(pktbuf_t) + 1;
-        free(s_idx);
-        s_idx = malloc(s_span * sizeof(size_t));
-        for (size_t i = 0; i < n; i++) s_idx[((size_t)all[i] - lo) / sizeof(pktbuf_t)] = i;
+/* Packet index of each buffer of a run: `all` holds the run's buffers in packet order (distinct
+ * pool slots); built once per run, after the worker is done (a cache keyed on the array's address
+ * could outlive it: the next run's malloc may hand back the same address with other buffers). */
+typedef struct {
+    size_t lo, span, *idx;
+} buf_index_t;
+static int buf_index_build(buf_index_t *x, pktbuf_t *const *all, size_t n) {
+    size_t lo = (size_t)-1, hi = 0;
+    for (size_t i = 0; i < n; i++) {
+        const size_t a = (size_t)all[i];
+        lo = a < lo ? a : lo;
+        hi = a > hi ? a : hi;
     }
-    return s_idx[((size_t)b - s_lo) / sizeof(pktbuf_t)];
+    x->lo = lo;
+    x->span = n ? (hi - lo) / sizeof(pktbuf_t) + 1 : 0;
+    x->idx = malloc((x->span ? x->span : 1) * sizeof(size_t));
+    if (!x->idx) return -1;
+    for (size_t i = 0; i < n; i++) x->idx[((size_t)all[i] - lo) / sizeof(pktbuf_t)] = i;
+    return 0;
+}
+static size_t index_of(const buf_index_t *x, const pktbuf_t *b) {
+    return x->idx[((size_t)b - x->lo) / sizeof(pktbuf_t)];
 }
 
 /*
@@ -242,6 +246,18 @@ static size_t index_of(pktbuf_t *const *all, size_t n, const pktbuf_t *b) {
  * pushes the rest; stats_a receives the old rule_stats array as it was at the swap, and
  * rule_stats the new one (cap_b entries).
  */
+/* UPE_DROPIN_BACKTRACE=1: a fault inside the harness prints the native frames (addresses map to
+ * the in-tree .so files with addr2line) before the process dies */
+static void on_fault(int sig) {
+    void *fr[48];
+    const int k = backtrace(fr, 48);
+    static const char msg[] = "upe_dropin: fatal signal, native frames:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(fr, k, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
                    const upe_arp_entry_t *arp, size_t arp_cap, const upe_ndp_entry_t *ndp,
                    size_t ndp_cap, const uint8_t eth_addr[6], uint32_t ip4_addr,
@@ -251,6 +267,10 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
                    const upe_rule_t *rules_b, size_t nrules_b, size_t cap_b, size_t at,
                    upe_rule_stat_t *stats_a, size_t log_cap, uint32_t *pops, uint32_t *sizes,
                    uint32_t *tx, uint32_t *replies, uint64_t log_n[4]) {
+    if (getenv("UPE_DROPIN_BACKTRACE")) {
+        signal(SIGSEGV, on_fault);
+        signal(SIGBUS, on_fault);
+    }
     rule_table_t *rt = malloc(sizeof *rt);
     if (!rt || rule_table_init(rt, capacity) != 0) return -1;
     for (size_t i = 0; i < nrules; i++)
@@ -377,8 +397,11 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     if (out_arp && arp_cap) memcpy(out_arp, arpt.entries, arp_cap * sizeof(arp_entry_t));
     if (out_ndp && ndp_cap) memcpy(out_ndp, ndpt.entries, ndp_cap * sizeof(ndp_entry_t));
     if (log_cap) {
-        for (size_t k = 0; k < g_log_nf; k++) tx[k] = (uint32_t)index_of(all, n, lf[k]);
-        for (size_t k = 0; k < g_log_nr; k++) replies[k] = (uint32_t)index_of(all, n, lr[k]);
+        buf_index_t bx;
+        if (buf_index_build(&bx, all, n) != 0) return -1;
+        for (size_t k = 0; k < g_log_nf; k++) tx[k] = (uint32_t)index_of(&bx, lf[k]);
+        for (size_t k = 0; k < g_log_nr; k++) replies[k] = (uint32_t)index_of(&bx, lr[k]);
+        free(bx.idx);
         log_n[0] = g_log_np;
         log_n[1] = g_log_nb;
         log_n[2] = g_log_nf;
