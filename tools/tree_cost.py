@@ -1,0 +1,88 @@
+"""Wave-level cost model of the decision-tree walk (round 5 design tool, CPU only).
+
+  python tools/tree_cost.py [--n 65536] [cases...]     cases: CF C6 C3 (config C flows / v6fwd / seed 3)
+
+Per 64-packet wave (the kernel's chunk): the walk's loop iterations (ILP groups of 3 trees, each
+as long as the wave's deepest walk in it) and the leaf loop's iterations, tree by tree (as built)
+or interleaved over a group's trees, from upe_tree_profile_host (the host walk of the same image:
+levels walked and leaf entries read per key and tree).  Environment knobs of the builder
+(UPE_GPU_TREE_DIMS, UPE_GPU_TREE_GROUP, UPE_GPU_TREE_BINTH) apply."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def keys_of(wl, n):
+    import oracle
+    from upe_amd import layout
+    from upe_amd.layout import FLOW_KEY_DTYPE
+    m = min(n, wl.n)
+    keys = np.zeros(m, FLOW_KEY_DTYPE)
+    offs, lens = layout.desc_offsets(wl.desc), layout.desc_lens(wl.desc)
+    for i in range(m):
+        o, ln = int(offs[i]), int(lens[i])
+        rc, k = oracle.parse(bytes(wl.frames[o:o + min(ln, 128)]), ln)
+        if rc == 0:
+            keys[i:i + 1].view(np.uint8)[:] = k
+    return keys
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("cases", nargs="*", default=["CF", "C6", "C3"])
+    args = ap.parse_args()
+    from upe_amd import gpu, synth
+    from upe_amd.layout import RULE_DTYPE, RULE_INDEX_INFO_DTYPE
+    lib = gpu.LIB
+    lib.upe_tree_profile_host.restype = ctypes.c_int
+    makers = {"CF": lambda: synth.config_c_flows(n=args.n), "C3": lambda: synth.config_c(n=args.n),
+              "C6": lambda: synth.config_c(n=args.n, v6_forwarding=True)}
+    P = ctypes.c_void_p
+    for c in args.cases:
+        wl = makers[c]()
+        keys = keys_of(wl, args.n)
+        n = len(keys)
+        rs = np.ascontiguousarray(wl.rules_sorted, dtype=RULE_DTYPE)
+        out = np.zeros(n, np.int64)
+        info = np.zeros(1, RULE_INDEX_INFO_DTYPE)
+        dep = np.zeros((n, 16), np.uint8)
+        stp = np.zeros((n, 16), np.uint8)
+        rc = lib.upe_tree_profile_host(rs.ctypes.data_as(P), ctypes.c_size_t(len(rs)),
+                                       keys.ctypes.data_as(P), ctypes.c_size_t(n),
+                                       out.ctypes.data_as(P), info.ctypes.data_as(P),
+                                       dep.ctypes.data_as(P), stp.ctypes.data_as(P))
+        assert rc == 0
+        nw = n // 64
+        dep = dep[:nw * 64].reshape(nw, 64, 16).astype(np.int32)
+        stp = stp[:nw * 64].reshape(nw, 64, 16).astype(np.int32)
+        ntw = int(max(info["trees"][0] & 0xFFFF, info["trees"][0] >> 16))
+        walk = leaf_seq = leaf_il = 0
+        for g0 in range(0, ntw, 3):
+            g = slice(g0, min(g0 + 3, ntw))
+            walk += dep[:, :, g].max(axis=2).max(axis=1).mean()
+            leaf_seq += stp[:, :, g].max(axis=1).sum(axis=1).mean()
+            leaf_il += stp[:, :, g].max(axis=2).max(axis=1).mean()
+        ilp = []
+        for k in range(1, 6):
+            it = sum(dep[:, :, g0:min(g0 + k, ntw)].max(axis=2).max(axis=1).mean()
+                     for g0 in range(0, ntw, k))
+            ilp.append(f"ilp{k}: {it:.1f} it / {it * k:.1f} slots")
+        print(f"{c}: walk " + ", ".join(ilp))
+        lane_walk = dep.sum(axis=2).mean()
+        lane_steps = stp.sum(axis=2).mean()
+        print(f"{c}: index {info[0].tolist()} trees/family {ntw}; per wave: walk iterations "
+              f"{walk:.1f}, leaf iterations tree-by-tree {leaf_seq:.1f} / interleaved {leaf_il:.1f}; "
+              f"per lane: levels {lane_walk:.1f}, leaf entries read {lane_steps:.2f}")
+
+
+if __name__ == "__main__":
+    main()

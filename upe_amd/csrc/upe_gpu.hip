@@ -311,6 +311,7 @@ constexpr int kTreeDims = 11;
 constexpr int kTreeIlp = UPE_TREE_ILP;   // trees a lane walks at once (tree_match)
 static_assert(kTreeIlp >= 1 && kTreeIlp <= 3, "tree_match spells out up to three walks");
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
+constexpr size_t kTreeMinReach = 64;   // (load_rules_impl: tree or scan)
 
 struct Args {
     uint8_t* frames;
@@ -838,10 +839,11 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
 #pragma unroll
             for (int u = 0; u < kTreeIlp; ++u) more = more || !(nds[u].x & 16u);
             if (!__any(more)) break;
-            auto advance = [&](uint2& ndr) {
+            // one level of each tree: every child index first, then the kTreeIlp node loads
+            // back to back (in flight together), then the selects that wait for them
+            auto child = [&](const uint2 nd) -> uint32_t {
                 // (bit selects, so that the key words stay in registers: a select between
                 // elements of s / d becomes an indexed load of a scratch copy otherwise)
-                const uint2 nd = ndr;
                 const uint32_t dim = nd.x & 15u;
                 const uint32_t m1 = 0u - (dim & 1u), m2 = 0u - ((dim >> 1) & 1u);
                 const uint32_t m4 = 0u - ((dim >> 2) & 1u), m8 = 0u - ((dim >> 3) & 1u);
@@ -850,63 +852,68 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                 uint32_t v = vsel(m4, da, sa);
                 if (is6) v = bswap32(v);
                 v = vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), v);
-                const bool leaf = (nd.x & 16u) != 0u;
-                const uint2 nx = N[leaf ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u)];
-                ndr = leaf ? nd : nx;
+                return (nd.x & 16u) ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u);
             };
+            uint32_t ix0 = child(nds[0]), ix1 = 0, ix2 = 0;
+            if constexpr (kTreeIlp > 1) ix1 = child(nds[1]);
+            if constexpr (kTreeIlp > 2) ix2 = child(nds[2]);
+            const uint2 nx0 = N[ix0];
+            uint2 nx1 = nx0, nx2 = nx0;
+            if constexpr (kTreeIlp > 1) nx1 = N[ix1];
+            if constexpr (kTreeIlp > 2) nx2 = N[ix2];
             // (spelled out: the compiler would not unroll a loop over the trees here)
-            advance(nds[0]);
-            if constexpr (kTreeIlp > 1) advance(nds[1]);
-            if constexpr (kTreeIlp > 2) advance(nds[2]);
+            if (!(nds[0].x & 16u)) nds[0] = nx0;
+            if constexpr (kTreeIlp > 1) if (!(nds[1].x & 16u)) nds[1] = nx1;
+            if constexpr (kTreeIlp > 2) if (!(nds[2].x & 16u)) nds[2] = nx2;
         }
         for (int u = 0; u < kTreeIlp; ++u) {   // the leaves, tree by tree
-        uint2 nd = nds[0];
+            uint2 nd = nds[0];
 #pragma unroll
-        for (int q = 1; q < kTreeIlp; ++q)   // (selects: nds stays in registers)
-            if (u == q) nd = nds[q];
-        const uint32_t cnt = nd.x >> 5;
-        bool look = cnt != 0u;
-        for (uint32_t j = 0; __any(look); ++j) {
-            if (look) {
-                const uint32_t e = E[nd.y + j];
-                const uint32_t p = e & 0x7FFFFFFFu;
-                if (p >= best) {
-                    look = false;   // the lists ascend: nothing later in this leaf can win
-                } else {
-                    uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
-                    const bool cov = (e >> 31) != 0u;
-                    if (is6 && a.fam6_lds) {
-                        const uint4* f = l6 + kFamV6Stride * p;
-                        e0 = f[0];
-                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
-                    } else if (is6) {
-                        const uint4* f = g6 + (size_t)kFamV6Stride * p;
-                        e0 = f[0];
-                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
-                    } else if (a.fam4_lds) {
-                        const uint4* f = l4 + 2 * p;
-                        e0 = f[0];
-                        if (!cov) e1 = f[1];
+            for (int q = 1; q < kTreeIlp; ++q)   // (selects: nds stays in registers)
+                if (u == q) nd = nds[q];
+            const uint32_t cnt = nd.x >> 5;
+            bool look = cnt != 0u;
+            for (uint32_t j = 0; __any(look); ++j) {
+                if (look) {
+                    const uint32_t e = E[nd.y + j];
+                    const uint32_t p = e & 0x7FFFFFFFu;
+                    if (p >= best) {
+                        look = false;   // the lists ascend: nothing later in this leaf can win
                     } else {
-                        const uint4* f = a.fam + 2 * (size_t)p;
-                        e0 = f[0];
-                        if (!cov) e1 = f[1];
-                    }
-                    uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
-                                 ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
-                    // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3 (zero words for IPv4 entries)
-                    x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
-                         ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
-                    if (cov || x == 0u) {
-                        best = p;
-                        bact = e0.z;
-                        look = false;
-                    } else if (j + 1u >= cnt) {
-                        look = false;
+                        uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
+                        const bool cov = (e >> 31) != 0u;
+                        if (is6 && a.fam6_lds) {
+                            const uint4* f = l6 + kFamV6Stride * p;
+                            e0 = f[0];
+                            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                        } else if (is6) {
+                            const uint4* f = g6 + (size_t)kFamV6Stride * p;
+                            e0 = f[0];
+                            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                        } else if (a.fam4_lds) {
+                            const uint4* f = l4 + 2 * p;
+                            e0 = f[0];
+                            if (!cov) e1 = f[1];
+                        } else {
+                            const uint4* f = a.fam + 2 * (size_t)p;
+                            e0 = f[0];
+                            if (!cov) e1 = f[1];
+                        }
+                        uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                                     ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
+                        // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3 (zero words for IPv4 entries)
+                        x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+                             ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+                        if (cov || x == 0u) {
+                            best = p;
+                            bact = e0.z;
+                            look = false;
+                        } else if (j + 1u >= cnt) {
+                            look = false;
+                        }
                     }
                 }
             }
-        }
         }
     }
     if (__any(active && best == kNone)) {
@@ -3345,7 +3352,8 @@ struct TreeImage {
 // contiguous).  rules: the family list's entries in list order.  Returns false when the node
 // budget or the leaf-length limit is exceeded (the table then keeps the linear scan).
 bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_t>& members,
-                       int fam_slot, uint32_t binth, size_t node_budget, TreeImage& img) {
+                       int fam_slot, uint32_t binth, size_t node_budget, TreeImage& img,
+                       uint32_t dims = (1u << kTreeDims) - 1u) {
     struct Task {
         uint32_t node;
         uint32_t depth;
@@ -3388,6 +3396,7 @@ bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_
         uint32_t best_t = 0, best_max = n, best_sum = 2 * n;
         if (n > binth && !covers[0]) {
             for (int d = 0; d < kTreeDims; ++d) {
+                if (!(dims >> d & 1u)) continue;
                 los.clear();
                 his.clear();
                 bool split = false;
@@ -3510,8 +3519,9 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
             if (*def == kNone) *def = (uint32_t)i;
         }
     }
+    // rules after the family's first catch-all are never a first match: no tree's
     std::vector<std::vector<uint32_t>> groups(ng + 1);
-    for (size_t i = 0; i < n; ++i)
+    for (size_t i = 0; i < n && i < *def; ++i)
         if (grp[i] >= 0) groups[grp[i]].push_back((uint32_t)i);
     for (int g = 0; g < ng; ++g)   // small groups share one tree (kept in list order)
         if (!groups[g].empty() && groups[g].size() < kTreeMinGroup) {
@@ -3526,7 +3536,11 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
         const size_t n0 = img.nodes.size(), e0 = img.leaves.size();
         // (large groups: longer leaves, or nested prefixes multiply the leaves)
         const uint32_t bt = members.size() > 4096 ? std::max(binth, 16u) : binth;
-        const bool ok = build_tree_family(R, members, fam_slot, bt, node_budget, img);
+        const char* dm = getenv("UPE_GPU_TREE_DIMS");   // experiment: "field" = own field only
+        uint32_t dims = (1u << kTreeDims) - 1u;
+        if (dm && dm[0] == 'f' && !by_word && g < ng)
+            dims = g == 0 ? 0xFu : g == 1 ? 0xF0u : 1u << (g + 6);
+        const bool ok = build_tree_family(R, members, fam_slot, bt, node_budget, img, dims);
         if (getenv("UPE_GPU_VERBOSE"))
             fprintf(stderr, "upe_gpu: tree family %d group %d: %zu rules, %zu nodes, %zu leaf entries%s\n",
                     fam_slot ? 6 : 4, g, members.size(), img.nodes.size() - n0,
@@ -3576,17 +3590,27 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
 uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
                         const std::vector<RuleV6>& v6, const std::vector<uint32_t>& list, bool is6,
                         const uint32_t kv[kTreeDims], uint32_t k0, uint32_t k1, const uint32_t s[4],
-                        const uint32_t d[4]) {
+                        const uint32_t d[4], uint8_t* prof_depth = nullptr,
+                        uint8_t* prof_steps = nullptr) {
     const uint2 dir = img.nodes[0], dflt = img.nodes[1];
     const uint32_t nt = is6 ? dir.y : dir.x, first = 2u + (is6 ? dir.x : 0u);
     uint32_t best = kNone;
     for (uint32_t t = 0; t < nt; ++t) {
         uint2 nd = img.nodes[first + t];
-        while (!(nd.x & 16u)) nd = img.nodes[(nd.x >> 5) + (kv[nd.x & 15u] >= nd.y ? 1u : 0u)];
+        uint32_t depth = 0;
+        while (!(nd.x & 16u)) {
+            nd = img.nodes[(nd.x >> 5) + (kv[nd.x & 15u] >= nd.y ? 1u : 0u)];
+            ++depth;
+        }
         const uint32_t cnt = nd.x >> 5;
+        if (prof_depth && t < 16) {
+            prof_depth[t] = (uint8_t)std::min(depth, 255u);
+            prof_steps[t] = 0;
+        }
         for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t e = img.leaves[nd.y + j];
             const uint32_t pos = e & 0x7FFFFFFFu;
+            if (prof_steps && t < 16 && prof_steps[t] < 255) ++prof_steps[t];
             if (pos >= best) break;
             bool hit = (e >> 31) != 0;
             if (!hit) {
@@ -3821,8 +3845,11 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
         }
     }
     // Linear-scan tables past kSmallRules without a tuple-space index: the decision tree over the
-    // family lists (kTreeDims comment), unless it outgrows its node budget (UPE_GPU_TREE: 0 = never,
-    // diagnostic; UPE_GPU_TREE_BINTH: rules per leaf before a split)
+    // family lists (kTreeDims comment), unless it outgrows its node budget, or a scan never gets
+    // far: both families' lists reach their first catch-all within kTreeMinReach entries (the
+    // scan's cost is then bounded by that, and its wave-uniform scalar loads beat the walk:
+    // seed-3 config C 38.1 vs 46.5 us).  UPE_GPU_TREE: 0 = never, 1 = whenever it builds
+    // (diagnostics); UPE_GPU_TREE_BINTH: rules per leaf before a split.
     bool tree_ok = false;
     std::vector<uint4> timg;
     TreeImage t;
@@ -3836,7 +3863,11 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
             memcpy(timg.data(), t.nodes.data(), t.nodes.size() * sizeof(uint2));
             memcpy(reinterpret_cast<uint32_t*>(timg.data()) + 2 * t.nodes.size(), t.leaves.data(),
                    t.leaves.size() * sizeof(uint32_t));
-            tree_ok = true;
+            // the list entries a scan can reach: up to the family's first catch-all (node 1)
+            const uint2 dflt = t.nodes[1];
+            const size_t reach = std::max(dflt.x == kNone ? l4.size() : (size_t)dflt.x + 1,
+                                          dflt.y == kNone ? l6.size() : (size_t)dflt.y + 1);
+            tree_ok = reach > kTreeMinReach || (tf && tf[0] == '1');
         }
     }
 
@@ -3971,12 +4002,26 @@ extern "C" int upe_gpu_rule_index_info(upe_gpu_ctx_t* c, upe_rule_index_info_t* 
     return 0;
 }
 
+extern "C" int upe_tree_profile_host(const upe_rule_t* rules, size_t count,
+                                     const upe_flow_key_t* keys, size_t n, int64_t* out,
+                                     upe_rule_index_info_t* info, uint8_t* prof_depth,
+                                     uint8_t* prof_steps);
+
 // rule_table_match (reference src/rule_table.c:163-176) for a batch of keys on the host, through
 // the decision tree the GPU path builds for the same table (tree_walk_host: the device's walk bit
 // for bit), or the family lists' linear first match when the table gets no tree.
 extern "C" int upe_rules_match_host(const upe_rule_t* rules, size_t count,
                                     const upe_flow_key_t* keys, size_t n, int64_t* out,
                                     upe_rule_index_info_t* info) {
+    return upe_tree_profile_host(rules, count, keys, n, out, info, nullptr, nullptr);
+}
+
+// (diagnostic, not part of the ABI) the same, and per key and tree of its family (first 16):
+// levels walked (prof_depth[16 * i + t]) and leaf entries read (prof_steps[16 * i + t])
+extern "C" int upe_tree_profile_host(const upe_rule_t* rules, size_t count,
+                                     const upe_flow_key_t* keys, size_t n, int64_t* out,
+                                     upe_rule_index_info_t* info, uint8_t* prof_depth,
+                                     uint8_t* prof_steps) {
     if ((count && !rules) || (n && (!keys || !out))) return fail("null argument");
     const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;
     std::vector<RuleV4> v4;
@@ -4025,7 +4070,9 @@ extern "C" int upe_rules_match_host(const upe_rule_t* rules, size_t count,
         const std::vector<uint32_t>& list = is6 ? l6 : l4;
         uint32_t pos = kNone;
         if (tree) {
-            pos = tree_walk_host(t, v4, v6, list, is6, kv, k0, k1, sw, dw);
+            pos = tree_walk_host(t, v4, v6, list, is6, kv, k0, k1, sw, dw,
+                                 prof_depth ? prof_depth + 16 * i : nullptr,
+                                 prof_steps ? prof_steps + 16 * i : nullptr);
         } else {
             for (size_t j = 0; j < list.size() && pos == kNone; ++j) {
                 const RuleV4& r = v4[list[j]];
