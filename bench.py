@@ -287,7 +287,7 @@ def dropin_pipeline(local: list | None, seconds: float = 2.0, device: int = 0) -
     cpus_all = [c for c in (local or []) if c in ALLOWED_CPUS] or ALLOWED_CPUS
     legs = []
     for pool, ring in ((8192, 1024), (262144, 32768)):
-        for gpu, mapped, workers in ((0, 0, 1), (0, 0, 4), (1, 1, 1), (1, 0, 1)):
+        for gpu, mapped, workers in ((0, 0, 1), (0, 0, 4), (1, 1, 1), (1, 1, 2), (1, 0, 1)):
             cpus = (ctypes.c_int * (1 + workers))(*[cpus_all[k % len(cpus_all)]
                                                     for k in range(1 + workers)])
             out = (ctypes.c_double * 5)()
@@ -543,8 +543,9 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
     issue rate (SURVEY.md §8(d) expected the rule work to bound it; SQ_INSTS_VALU per launch,
     tools/pmc_valu.py, against 1024 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz) and the
     bytes requested past L2 (2 x FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.py) against HBM;
-    `bound` names the one nearer its peak (measured round 4: the bytes, ~0.8 of 8 TB/s, VALU
-    ~0.33).  The algorithmic-bytes fraction follows.  Not `value`."""
+    the top-level roofline is the algorithmic-bytes fraction (bytes the path must move / step
+    time) with the counted bytes as its traffic (round 4 measured the counted bytes at ~0.8 of
+    8 TB/s, VALU ~0.33).  Not `value`."""
     from upe_amd import gpu, synth
 
     t_gen = time.perf_counter()
@@ -617,10 +618,13 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
         hbm.update({"achieved": None, "frac": None})
     roof["valu"] = valu
     roof["hbm"] = hbm
-    fv, fh = valu.get("frac") or 0.0, hbm.get("frac") or 0.0
-    top = hbm if fh >= fv else valu
-    roof.update({"bound": "hbm" if top is hbm else "valu", "achieved": top.get("achieved"),
-                 "peak": top["peak"], "unit": top["unit"], "frac": top.get("frac")})
+    # the headline fraction is the algorithmic one (the bytes the path must move, per step time),
+    # with the counted past-L2 bytes as its traffic, as for the other legs; the VALU issue rate
+    # and the counted-bytes rate stay beside it (valu / hbm)
+    roof.update({"bound": "hbm", "achieved": hbm["algorithmic"]["achieved"], "peak": HBM_PEAK_GBPS,
+                 "unit": "GB/s", "frac": hbm["algorithmic"]["frac"], "traffic": traffic,
+                 "algorithmic_bytes_per_packet": hbm["algorithmic"]["bytes_per_packet"],
+                 "traffic_bytes_per_packet": round(traffic / n, 2) if traffic else None})
     return {"workload": WORKLOADS["D"] + f", {n} packets per step", "value": round(n * steps / elapsed / 1e6, 2),
             "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps,
             "rule_index": "tuple space" if kind == 1 else "linear scan",
@@ -780,8 +784,9 @@ def main() -> None:
 
     # this rank's static shard: a full batch of the configuration, its own seed
     make = {"A": synth.config_a, "B": synth.config_b, "C": synth.config_c_flows,
+            "C3": synth.config_c, "C6": lambda **k: synth.config_c(v6_forwarding=True, **k),
             "D": synth.config_d}[args.config]
-    kw = {"seed": {"A": 1, "B": 2, "C": 3, "D": 4}[args.config] + 1000 * rank}
+    kw = {"seed": {"A": 1, "B": 2, "C": 3, "C3": 3, "C6": 3, "D": 4}[args.config] + 1000 * rank}
     if args.packets:
         kw["n"] = args.packets
     wl = make(**kw)

@@ -7,6 +7,7 @@ set -e
 cfg=${1:-B}; shift || true
 mode=${1:-emit}; shift || true
 groups=${*:-fetch write sq clk}
+lab=${PMC_LABEL:-$cfg}   # the output name (gpurun_out/pmc_<label>_<mode>/, tools/pmc_traffic.py <label>)
 steps="--steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline --no-hbm-probe --host-reps 0 --config $cfg --mode $mode --no-other-mode --no-imix --ring 0 --config-d-steps 0"
 for g in $groups; do
   case $g in
@@ -22,5 +23,5 @@ for g in $groups; do
     rdreq) ctr="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" ;;
     dram) ctr="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum" ;;
   esac
-  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${cfg}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${cfg}_${mode}_$g.log 2>&1 || { echo "pass $g failed rc=$?"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${lab}_$mode/$g -o p --output-format csv -- python bench.py $steps > gpurun_out/pmc_${lab}_${mode}_$g.log 2>&1 || { echo "pass $g failed rc=$?"; exit 1; }
 done

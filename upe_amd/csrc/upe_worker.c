@@ -32,11 +32,15 @@
  * Two ways to get a batch to the GPU (cfg->pool_base): copy each frame's header window into
  * pinned staging, ship it with the descriptors, classify in emit mode and bring back the verdicts
  * and 16-byte records (applied to the caller's buffers in the walk, upe_hdr_apply) — or leave the
- * frames where they are in a registered pool and let the kernel classify and rewrite them there
- * (upe_gpu_process_mapped, nothing copied).
+ * frames where they are in a registered pool, let the kernel read them there over the link and
+ * write the verdicts and records into pinned host memory (upe_gpu_process_mapped_emit, nothing
+ * copied), the records applied in the walk.  (Rewriting the frames in the pool from the GPU
+ * instead, upe_gpu_process_mapped, measured 50 vs 66 Mpps for one worker thread on the reference
+ * benchmark: the link writes evict the frame lines the walk and pktbuf_free then touch.)
  */
 #define _GNU_SOURCE
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #include <time.h>
 
@@ -89,7 +93,18 @@ typedef struct {
     void *tx_bufs[UPE_TX_BATCH_MAX];
     int tx_count;
     upe_counters_t c;
+    /* UPE_WORKER_PROFILE=1 (diagnostic): where the loop's time goes, printed at the end */
+    int inplace;       /* mapped mode, UPE_WORKER_MAPPED_INPLACE=1 (diagnostic): the kernel
+                          rewrites the frames in the pool instead of emitting records */
+    int prof;
+    uint64_t t_wait, t_walk, t_launch, n_batches;
 } loop_t;
+
+static uint64_t mono_ns(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 static uint8_t at(const uint8_t *d, size_t len, size_t k) { return k < len ? d[k] : 0; }
 
@@ -146,8 +161,11 @@ static void flush_tx(loop_t *L) {
 static int launch(loop_t *L, int k) {
     slot_t *S = &L->s[k];
     const size_t n = S->n;
+    const uint64_t t0 = L->prof ? mono_ns() : 0;
     int rc;
-    if (L->pool) {
+    if (L->pool && !L->inplace) {
+        rc = upe_gpu_process_mapped_emit(L->ctx, L->pool, S->desc, S->verdict, S->rec, n, NULL);
+    } else if (L->pool) {
         rc = upe_gpu_process_mapped(L->ctx, L->pool, S->desc, S->verdict, n, NULL);
     } else {
         rc = upe_gpu_memcpy_h2d(L->ctx, S->d_win, S->win, n * WIN, NULL);
@@ -161,6 +179,10 @@ static int launch(loop_t *L, int k) {
     }
     if (rc == 0) rc = upe_gpu_mark(L->ctx, k);
     S->busy = rc == 0;
+    if (L->prof) {
+        L->t_launch += mono_ns() - t0;
+        L->n_batches++;
+    }
     return rc;
 }
 
@@ -169,16 +191,27 @@ static int launch(loop_t *L, int k) {
  * before anything else is launched. */
 static int walk(loop_t *L, int k) {
     slot_t *S = &L->s[k];
+    const uint64_t t0 = L->prof ? mono_ns() : 0;
     if (upe_gpu_mark_wait(L->ctx, k) != 0) return -1;
+    const uint64_t t1 = L->prof ? mono_ns() : 0;
     const size_t n = S->n;
     size_t rec = 0; /* window mode: the next forwarded packet's record (compacted per 64) */
     for (size_t i = 0; i < n; i++) {
         void *b = S->bufs[i];
         uint8_t *d = S->data[i];
+        /* the first line of a frame a few packets ahead, for the record's writes and the
+         * handle's release (the line left this core's caches since the gather) */
+        if (i + 16 < n) __builtin_prefetch(S->data[i + 16], 1);
         const size_t len = (size_t)(S->desc[i] & 0xFFFFu);
         const uint32_t v = S->verdict[i];
         const uint32_t code = UPE_VERDICT_CODE(v);
-        if (!L->pool) {
+        if (L->pool && !L->inplace) {
+            /* mapped mode: the forwarded frames' records applied here, where the frame's first
+             * line is still in this core's cache from the gather (the kernel only reads the pool;
+             * an answered ARP request it rewrote in place) */
+            if ((i & 63u) == 0) rec = i;
+            if (code == UPE_V_FWD) upe_hdr_apply(d, &S->rec[rec++]);
+        } else if (!L->pool) {
             /* window mode: the rewritten bytes into the caller's buffer (an answered ARP
              * request ends a cut batch, so nothing is queued behind it: a synchronous copy) */
             if ((i & 63u) == 0) rec = i;
@@ -228,6 +261,11 @@ static int walk(loop_t *L, int k) {
     S->n = 0;
     S->cut = 0;
     S->busy = 0;
+    if (L->prof) {
+        const uint64_t t2 = mono_ns();
+        L->t_wait += t1 - t0;
+        L->t_walk += t2 - t1;
+    }
     if (cut && L->ops->load_neigh(L->user, L->ctx) != 0) return -1;
     if (L->ops->publish) L->ops->publish(L->user, L->ctx, &L->c);
     return 0;
@@ -291,6 +329,10 @@ static int alloc_slots(loop_t *L) {
         S->desc = upe_gpu_host_alloc(L->cap * sizeof(uint64_t));
         S->verdict = upe_gpu_host_alloc(L->cap * sizeof(uint32_t));
         if (!S->bufs || !S->data || !S->desc || !S->verdict) return -1;
+        if (L->pool && !L->inplace) {
+            S->rec = upe_gpu_host_alloc(L->cap * sizeof(upe_hdr_rec_t));
+            if (!S->rec) return -1;
+        }
         if (!L->pool) {
             S->win = upe_gpu_host_alloc(L->cap * WIN + UPE_FRAME_TAIL);
             S->rec = upe_gpu_host_alloc(L->cap * sizeof(upe_hdr_rec_t));
@@ -327,6 +369,11 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
     L.pool = cfg ? cfg->pool_base : NULL;
     L.pool_bytes = cfg ? cfg->pool_bytes : 0;
     L.o = -1;
+    const char *pe = getenv("UPE_WORKER_PROFILE");
+    L.prof = pe && pe[0] == '1';
+    const char *pi = getenv("UPE_WORKER_MAPPED_INPLACE");
+    L.inplace = pi && pi[0] == '1';
+    const uint64_t t_start = L.prof ? mono_ns() : 0;
     const unsigned idle = cfg && cfg->idle_ns ? cfg->idle_ns : 1000;
     const struct timespec nap = {(time_t)(idle / 1000000000u), (long)(idle % 1000000000u)};
     if (L.burst > UPE_TX_BATCH_MAX) return upe_gpu_set_last_error("burst exceeds UPE_TX_BATCH_MAX");
@@ -371,10 +418,17 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
         L.c.pkts_in += k; /* src/worker.c:280 */
         L.bq[(L.bq_head + L.bq_len) % L.bq_cap] = k;
         L.bq_len++;
+        /* the burst's frames first, their first lines requested together (the producer wrote
+         * them on another core: one cross-core transfer each, overlapped) */
+        uint8_t *bd[UPE_TX_BATCH_MAX];
+        for (unsigned j = 0; j < k; j++) {
+            bd[j] = ops->data(user, burst[j]);
+            __builtin_prefetch(bd[j]);
+        }
         for (unsigned j = 0; j < k; j++) {
             G = &L.s[L.g];
             void *b = burst[j];
-            uint8_t *d = ops->data(user, b);
+            uint8_t *d = bd[j];
             const size_t len = ops->len(user, b);
             if (L.pool) {
                 const size_t off = (size_t)(d - L.pool);
@@ -408,6 +462,13 @@ fail:
     rc = -1;
     drain(&L);
 out:
+    if (L.prof)
+        fprintf(stderr, "upe_worker: %.3f s total, %llu batches (%.0f packets each): launch %.3f s, "
+                "GPU wait %.3f s, walk %.3f s, rest (pop + gather + idle) %.3f s\n",
+                (mono_ns() - t_start) * 1e-9, (unsigned long long)L.n_batches,
+                L.n_batches ? (double)L.c.pkts_in / (double)L.n_batches : 0.0, L.t_launch * 1e-9,
+                L.t_wait * 1e-9, L.t_walk * 1e-9,
+                (mono_ns() - t_start - L.t_launch - L.t_wait - L.t_walk) * 1e-9);
     if (counters) *counters = L.c;
     free(L.bq);
     free_slots(&L);
