@@ -36,7 +36,8 @@ def main() -> None:
     from upe_amd import gpu, synth
 
     dev = torch.device("cuda:0")
-    makers = {"CF": lambda: synth.config_c_flows(), "C3": lambda: synth.config_c(),
+    makers = {"B": lambda: synth.config_b(), "CF": lambda: synth.config_c_flows(),
+              "C3": lambda: synth.config_c(),
               "C6": lambda: synth.config_c(v6_forwarding=True)}
     cache: dict = {}
     ref_verdict: dict = {}

@@ -305,11 +305,6 @@ constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 // then a copy of each tree's root, IPv4 first), the nodes, then the leaf entries; staged in LDS
 // when it fits beside the launch's other LDS data.
 constexpr int kTreeDims = 11;
-#ifndef UPE_TREE_ILP
-#define UPE_TREE_ILP 3
-#endif
-constexpr int kTreeIlp = UPE_TREE_ILP;   // trees a lane walks at once (tree_match)
-static_assert(kTreeIlp >= 1 && kTreeIlp <= 3, "tree_match spells out up to three walks");
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
 constexpr size_t kTreeMinReach = 64;   // (load_rules_impl: tree or scan)
 
@@ -807,12 +802,16 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
     return pos == kNone ? kNone : (is6 ? a.fam4 : 0u) + pos;
 }
 
-// First match through the decision-tree index (kTreeDims comment): for each tree of its
-// family's forest a lane walks to a leaf, then tests the leaf's rules in list order against their
+// First match through the decision-tree index (kTreeDims comment): for each of its family's five
+// field trees a lane walks to a leaf, then tests the leaf's rules in list order against their
 // FamTable entries (the flagged one without a test), stopping at its first match or at a
-// position no better than the best so far.  Walks are per lane (divergent loads: LDS when the
-// image is staged, else memory); the wave iterates as long as its deepest walk and its longest
-// leaf, tree by tree.  Returns the lane's FamTable index-array entry, as scan_fam.
+// position no better than the best so far.  A field's tree splits on that field's words only, so
+// each level compares one key word known before the walk (an address tree: one of the field's
+// four words, by the node's low dimension bits).  Walks are per lane (divergent loads: LDS when
+// the image is staged, else memory), three trees at a time (source address, source port,
+// protocol; then destination address, destination port), their node loads in flight together;
+// the wave iterates as long as its deepest walk and its longest leaf, tree by tree.  Returns the
+// lane's FamTable index-array entry, as scan_fam.
 template <bool kLdsTree>
 __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool is6, uint32_t k0,
                                                uint32_t k1, const uint32_t s[4], const uint32_t d[4],
@@ -821,100 +820,92 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint2* N = kLdsTree ? lnodes : a.tree;
     const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
     const uint2 dir = N[0];
-    const uint32_t ntw = __builtin_amdgcn_readfirstlane(dir.x > dir.y ? dir.x : dir.y);
     const uint32_t nt = active ? (is6 ? dir.y : dir.x) : 0u, first = 2u + (is6 ? dir.x : 0u);
-    // key word `dim`: address words raw (IPv6 byte-swapped below), ports and protocol from k0/k1
     const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
-    for (uint32_t t0 = 0; t0 < ntw; t0 += kTreeIlp) {
-        // kTreeIlp trees walked together: one node load per tree and level, all in flight at once
-        // (a lane whose walk of a tree has ended reloads the directory word, a broadcast)
-        uint2 nds[kTreeIlp];
-#pragma unroll
-        for (int u = 0; u < kTreeIlp; ++u)   // lanes without a tree t0 + u: an empty leaf
-            nds[u] = t0 + u < nt ? N[first + t0 + u] : make_uint2(16u, 0u);
-        for (;;) {
-            bool more = false;
-#pragma unroll
-            for (int u = 0; u < kTreeIlp; ++u) more = more || !(nds[u].x & 16u);
-            if (!__any(more)) break;
-            // one level of each tree: every child index first, then the kTreeIlp node loads
-            // back to back (in flight together), then the selects that wait for them
-            auto child = [&](const uint2 nd) -> uint32_t {
-                // (bit selects, so that the key words stay in registers: a select between
-                // elements of s / d becomes an indexed load of a scratch copy otherwise)
-                const uint32_t dim = nd.x & 15u;
-                const uint32_t m1 = 0u - (dim & 1u), m2 = 0u - ((dim >> 1) & 1u);
-                const uint32_t m4 = 0u - ((dim >> 2) & 1u), m8 = 0u - ((dim >> 3) & 1u);
-                const uint32_t sa = vsel(m2, vsel(m1, s[3], s[2]), vsel(m1, s[1], s[0]));
-                const uint32_t da = vsel(m2, vsel(m1, d[3], d[2]), vsel(m1, d[1], d[0]));
-                uint32_t v = vsel(m4, da, sa);
-                if (is6) v = bswap32(v);
-                v = vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), v);
-                return (nd.x & 16u) ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u);
-            };
-            uint32_t ix0 = child(nds[0]), ix1 = 0, ix2 = 0;
-            if constexpr (kTreeIlp > 1) ix1 = child(nds[1]);
-            if constexpr (kTreeIlp > 2) ix2 = child(nds[2]);
-            const uint2 nx0 = N[ix0];
-            uint2 nx1 = nx0, nx2 = nx0;
-            if constexpr (kTreeIlp > 1) nx1 = N[ix1];
-            if constexpr (kTreeIlp > 2) nx2 = N[ix2];
-            // (spelled out: the compiler would not unroll a loop over the trees here)
-            if (!(nds[0].x & 16u)) nds[0] = nx0;
-            if constexpr (kTreeIlp > 1) if (!(nds[1].x & 16u)) nds[1] = nx1;
-            if constexpr (kTreeIlp > 2) if (!(nds[2].x & 16u)) nds[2] = nx2;
-        }
-        for (int u = 0; u < kTreeIlp; ++u) {   // the leaves, tree by tree
-            uint2 nd = nds[0];
-#pragma unroll
-            for (int q = 1; q < kTreeIlp; ++q)   // (selects: nds stays in registers)
-                if (u == q) nd = nds[q];
-            const uint32_t cnt = nd.x >> 5;
-            bool look = cnt != 0u;
-            for (uint32_t j = 0; __any(look); ++j) {
-                if (look) {
-                    const uint32_t e = E[nd.y + j];
-                    const uint32_t p = e & 0x7FFFFFFFu;
-                    if (p >= best) {
-                        look = false;   // the lists ascend: nothing later in this leaf can win
+    const uint2 empty = make_uint2(16u, 0u);
+    // The leaf of one tree: its rules in list order until a match or a position >= best.
+    auto leaf_tests = [&](const uint2 nd) {
+        const uint32_t cnt = nd.x >> 5;
+        bool look = cnt != 0u;
+        for (uint32_t j = 0; __any(look); ++j) {
+            if (look) {
+                const uint32_t e = E[nd.y + j];
+                const uint32_t p = e & 0x7FFFFFFFu;
+                if (p >= best) {
+                    look = false;   // the lists ascend: nothing later in this leaf can win
+                } else {
+                    uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
+                    const bool cov = (e >> 31) != 0u;
+                    if (is6 && a.fam6_lds) {
+                        const uint4* f = l6 + kFamV6Stride * p;
+                        e0 = f[0];
+                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                    } else if (is6) {
+                        const uint4* f = g6 + (size_t)kFamV6Stride * p;
+                        e0 = f[0];
+                        if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+                    } else if (a.fam4_lds) {
+                        const uint4* f = l4 + 2 * p;
+                        e0 = f[0];
+                        if (!cov) e1 = f[1];
                     } else {
-                        uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
-                        const bool cov = (e >> 31) != 0u;
-                        if (is6 && a.fam6_lds) {
-                            const uint4* f = l6 + kFamV6Stride * p;
-                            e0 = f[0];
-                            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
-                        } else if (is6) {
-                            const uint4* f = g6 + (size_t)kFamV6Stride * p;
-                            e0 = f[0];
-                            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
-                        } else if (a.fam4_lds) {
-                            const uint4* f = l4 + 2 * p;
-                            e0 = f[0];
-                            if (!cov) e1 = f[1];
-                        } else {
-                            const uint4* f = a.fam + 2 * (size_t)p;
-                            e0 = f[0];
-                            if (!cov) e1 = f[1];
-                        }
-                        uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
-                                     ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
-                        // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3 (zero words for IPv4 entries)
-                        x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
-                             ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
-                        if (cov || x == 0u) {
-                            best = p;
-                            bact = e0.z;
-                            look = false;
-                        } else if (j + 1u >= cnt) {
-                            look = false;
-                        }
+                        const uint4* f = a.fam + 2 * (size_t)p;
+                        e0 = f[0];
+                        if (!cov) e1 = f[1];
+                    }
+                    uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                                 ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
+                    // s1 s2 s3 sm1 | sm2 sm3 d1 d2 | d3 dm1 dm2 dm3 (zero words for IPv4 entries)
+                    x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+                         ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+                    if (cov || x == 0u) {
+                        best = p;
+                        bact = e0.z;
+                        look = false;
+                    } else if (j + 1u >= cnt) {
+                        look = false;
                     }
                 }
             }
         }
+    };
+    // one level of a tree: the child a key word picks (0 = stay: the directory word, a broadcast)
+    auto child = [](const uint2 nd, uint32_t v) -> uint32_t {
+        return (nd.x & 16u) ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u);
+    };
+    // an address field's word for a node: the key words big-endian for IPv6 (a prefix is then a
+    // range), IPv4's host-order word 0 and zeros; bit selects keep them in registers
+    auto addr_word = [](const uint2 nd, const uint32_t (&w)[4]) -> uint32_t {
+        const uint32_t m1 = 0u - (nd.x & 1u), m2 = 0u - ((nd.x >> 1) & 1u);
+        return vsel(m2, vsel(m1, w[3], w[2]), vsel(m1, w[1], w[0]));
+    };
+    for (int half = 0; half < 2; ++half) {
+        // half 0: source address, source port, protocol; half 1: destination address and port
+        uint32_t aw[4];
+        const uint32_t* src = half == 0 ? s : d;
+        aw[0] = is6 ? bswap32(src[0]) : src[0];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) aw[q] = is6 ? bswap32(src[q]) : 0u;
+        const uint32_t pv = half == 0 ? sp : dp;
+        uint2 na = nt ? N[first + (half == 0 ? 0u : 1u)] : empty;
+        uint2 nb = nt ? N[first + (half == 0 ? 2u : 3u)] : empty;
+        uint2 nc = nt && half == 0 ? N[first + 4u] : empty;
+        for (;;) {
+            const bool more = !(na.x & 16u) || !(nb.x & 16u) || !(nc.x & 16u);
+            if (!__any(more)) break;
+            const uint32_t ia = child(na, addr_word(na, aw));
+            const uint32_t ib = child(nb, pv);
+            const uint32_t ic = child(nc, pr);
+            const uint2 xa = N[ia], xb = N[ib], xc = N[ic];
+            if (!(na.x & 16u)) na = xa;
+            if (!(nb.x & 16u)) nb = xb;
+            if (!(nc.x & 16u)) nc = xc;
+        }
+        leaf_tests(na);
+        leaf_tests(nb);
+        if (half == 0) leaf_tests(nc);
     }
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
@@ -3468,31 +3459,27 @@ bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_
 }
 
 // One family's forest: its rules grouped by the key field (source address, destination address,
-// source port, destination port, protocol) whose word overlaps the fewest other rules of the list
-// (EffiCuts-style separation: a rule narrow only in its destination port is not copied into every
-// leaf of a tree that splits on addresses; an address prefix is exact on its leading words, so
-// one tree per address field splits on any of its words without copies), one tree per group,
-// every tree's rules in list order; groups of fewer than kTreeMinGroup rules share one tree.  A
-// key's first match is the smallest of its first matches in the trees (the groups partition the
-// list).  The family's rule that matches every key (the list's last entry, if any) is no tree's:
-// it is the answer when no tree has one (*def, its list position, else kNone).
+// source port, destination port, protocol) whose range overlaps the fewest other rules of the
+// list (EffiCuts-style separation: a rule narrow only in its destination port is not copied into
+// every leaf of a tree that splits on addresses), one tree per field, each split on its own field's
+// words only (so that a walk compares one known key word per level: tree_match), every tree's
+// rules in list order; a field no rule is narrowest in gets an empty tree.  A key's first match
+// is the smallest of its first matches in the trees (the groups partition the list).  The
+// family's first rule that matches every key is no tree's, nor is any rule after it: it is the
+// answer when no tree has one (*def, its list position, else kNone).  roots: kTreeFields entries.
 constexpr int kTreeFields = 5;
-constexpr size_t kTreeMinGroup = 8;
 int tree_field(int d) { return d < 4 ? 0 : d < 8 ? 1 : d - 6; }
+constexpr uint32_t kTreeFieldDims[kTreeFields] = {0xFu, 0xF0u, 1u << 8, 1u << 9, 1u << 10};
 bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
                          size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots,
                          uint32_t* def) {
     const size_t n = R.size();
     roots.clear();
     *def = kNone;
-    if (n == 0) return true;
     std::vector<int> grp(n, -1);
     std::vector<uint32_t> best(n, 0xFFFFFFFFu);
     std::vector<uint32_t> los(n), his(n);
-    const char* gm = getenv("UPE_GPU_TREE_GROUP");   // diagnostic: "word" = one group per key word
-    const bool by_word = gm && gm[0] == 'w';
-    const int ng = by_word ? kTreeDims : kTreeFields;
-    for (int d = 0; d < kTreeDims; ++d) {
+    for (int d = 0; d < kTreeDims && n > 0; ++d) {
         for (size_t i = 0; i < n; ++i) {
             los[i] = R[i].lo[d];
             his[i] = R[i].hi[d];
@@ -3506,7 +3493,7 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
             const uint32_t ov = (uint32_t)(a - b);
             if (ov < best[i]) {
                 best[i] = ov;
-                grp[i] = by_word ? d : tree_field(d);
+                grp[i] = tree_field(d);
             }
         }
     }
@@ -3514,35 +3501,29 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
         bool all = true;
         for (int d = 0; d < kTreeDims && all; ++d)
             all = (R[i].exact >> d & 1u) && R[i].lo[d] == 0 && R[i].hi[d] == kTreeWidth[d];
-        if (all) {   // matches every key of the family (the list ends with it)
+        if (all) {   // matches every key of the family
             grp[i] = -1;
             if (*def == kNone) *def = (uint32_t)i;
         }
     }
     // rules after the family's first catch-all are never a first match: no tree's
-    std::vector<std::vector<uint32_t>> groups(ng + 1);
+    std::vector<std::vector<uint32_t>> groups(kTreeFields);
     for (size_t i = 0; i < n && i < *def; ++i)
         if (grp[i] >= 0) groups[grp[i]].push_back((uint32_t)i);
-    for (int g = 0; g < ng; ++g)   // small groups share one tree (kept in list order)
-        if (!groups[g].empty() && groups[g].size() < kTreeMinGroup) {
-            groups[ng].insert(groups[ng].end(), groups[g].begin(), groups[g].end());
-            groups[g].clear();
-        }
-    std::sort(groups[ng].begin(), groups[ng].end());
-    for (int g = 0; g <= ng; ++g) {
+    for (int g = 0; g < kTreeFields; ++g) {
         const std::vector<uint32_t>& members = groups[g];
-        if (members.empty()) continue;
         roots.push_back((uint32_t)img.nodes.size());
+        if (members.empty()) {   // an empty leaf
+            img.nodes.push_back(make_uint2(16u, 0u));
+            continue;
+        }
         const size_t n0 = img.nodes.size(), e0 = img.leaves.size();
         // (large groups: longer leaves, or nested prefixes multiply the leaves)
         const uint32_t bt = members.size() > 4096 ? std::max(binth, 16u) : binth;
-        const char* dm = getenv("UPE_GPU_TREE_DIMS");   // experiment: "field" = own field only
-        uint32_t dims = (1u << kTreeDims) - 1u;
-        if (dm && dm[0] == 'f' && !by_word && g < ng)
-            dims = g == 0 ? 0xFu : g == 1 ? 0xF0u : 1u << (g + 6);
-        const bool ok = build_tree_family(R, members, fam_slot, bt, node_budget, img, dims);
+        const bool ok = build_tree_family(R, members, fam_slot, bt, node_budget, img,
+                                          kTreeFieldDims[g]);
         if (getenv("UPE_GPU_VERBOSE"))
-            fprintf(stderr, "upe_gpu: tree family %d group %d: %zu rules, %zu nodes, %zu leaf entries%s\n",
+            fprintf(stderr, "upe_gpu: tree family %d field %d: %zu rules, %zu nodes, %zu leaf entries%s\n",
                     fam_slot ? 6 : 4, g, members.size(), img.nodes.size() - n0,
                     img.leaves.size() - e0, ok ? "" : " (over budget)");
         if (!ok) return false;

@@ -353,7 +353,8 @@ class GpuWorker:
 
     def process_queue_emit(self, batches, stream=None) -> None:
         """upe_gpu_process_queue_emit over a list of (frames, desc, verdict, hdr, n) device
-        buffers (pointers or tensors): the worker loop with consecutive launches overlapped."""
+        buffers (pointers or tensors): the worker loop's resident batches, one launch each on the
+        context's stream, in order (the overlapped form was removed in round 4)."""
         arr = (QueueBatch * len(batches))(*[QueueBatch(_dev_ptr(f), _dev_ptr(d), _dev_ptr(v),
                                                        _dev_ptr(h), int(n))
                                             for f, d, v, h, n in batches])
