@@ -36,7 +36,15 @@ def main() -> None:
     from upe_amd import gpu, synth
 
     dev = torch.device("cuda:0")
+    def mixed_64k():
+        # the parity test's 64k-rule many-signature table over config C's traffic
+        wl = synth.config_c(seed=61)
+        wl.rules, wl.capacity = synth.mixed_table(1 << 16, 61), 1 << 16
+        return wl
+
     makers = {"B": lambda: synth.config_b(), "CF": lambda: synth.config_c_flows(),
+              "M64k": mixed_64k,
+              "F16k": lambda: synth.config_c_flows(seed=62, n_rules=1 << 14, max_cover=2.0 ** -18),
               "C3": lambda: synth.config_c(),
               "C6": lambda: synth.config_c(v6_forwarding=True)}
     cache: dict = {}

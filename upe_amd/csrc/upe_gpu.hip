@@ -805,11 +805,12 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
 // First match through the decision-tree index (kTreeDims comment): for each of its family's five
 // field trees a lane walks to a leaf, then tests the leaf's rules in list order against their
 // FamTable entries (the flagged one without a test), stopping at its first match or at a
-// position no better than the best so far.  A field's tree splits on that field's words only, so
-// each level compares one key word known before the walk (an address tree: one of the field's
-// four words, by the node's low dimension bits).  Walks are per lane (divergent loads: LDS when
-// the image is staged, else memory), three trees at a time (source address, source port,
-// protocol; then destination address, destination port), their node loads in flight together;
+// position no better than the best so far.  A field's tree splits on that field's words only (an
+// address tree also on the ports and the protocol), so each level compares one of a few key words
+// prepared before the walk (an address tree: one of its field's four words or a port word, by
+// the node's dimension bits).  Walks are per lane (divergent loads: LDS when
+// the image is staged, else memory), the deep trees together (source and destination address,
+// destination port), then the shallow ones (source port, protocol), node loads in flight together;
 // the wave iterates as long as its deepest walk and its longest leaf, tree by tree.  Returns the
 // lane's FamTable index-array entry, as scan_fam.
 template <bool kLdsTree>
@@ -875,29 +876,34 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     auto child = [](const uint2 nd, uint32_t v) -> uint32_t {
         return (nd.x & 16u) ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u);
     };
-    // an address field's word for a node: the key words big-endian for IPv6 (a prefix is then a
-    // range), IPv4's host-order word 0 and zeros; bit selects keep them in registers
-    auto addr_word = [](const uint2 nd, const uint32_t (&w)[4]) -> uint32_t {
+    // an address tree's key word for a node: one of its field's words (big-endian for IPv6, so
+    // that a prefix is a range; IPv4's host-order word 0 and zeros), or a port or the protocol
+    // (dimensions 8-10); bit selects keep them in registers
+    auto addr_word = [&](const uint2 nd, const uint32_t (&w)[4]) -> uint32_t {
         const uint32_t m1 = 0u - (nd.x & 1u), m2 = 0u - ((nd.x >> 1) & 1u);
-        return vsel(m2, vsel(m1, w[3], w[2]), vsel(m1, w[1], w[0]));
+        const uint32_t m8 = 0u - ((nd.x >> 3) & 1u);
+        const uint32_t aw = vsel(m2, vsel(m1, w[3], w[2]), vsel(m1, w[1], w[0]));
+        return vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), aw);
     };
-    for (int half = 0; half < 2; ++half) {
-        // half 0: source address, source port, protocol; half 1: destination address and port
-        uint32_t aw[4];
-        const uint32_t* src = half == 0 ? s : d;
-        aw[0] = is6 ? bswap32(src[0]) : src[0];
+    {
+        // the deep trees together (source and destination address, destination port), then the
+        // shallow ones (source port, protocol: few distinct values)
+        uint32_t ws[4], wd[4];
+        ws[0] = is6 ? bswap32(s[0]) : s[0];
+        wd[0] = is6 ? bswap32(d[0]) : d[0];
 #pragma unroll
-        for (int q = 1; q < 4; ++q) aw[q] = is6 ? bswap32(src[q]) : 0u;
-        const uint32_t pv = half == 0 ? sp : dp;
-        uint2 na = nt ? N[first + (half == 0 ? 0u : 1u)] : empty;
-        uint2 nb = nt ? N[first + (half == 0 ? 2u : 3u)] : empty;
-        uint2 nc = nt && half == 0 ? N[first + 4u] : empty;
+        for (int q = 1; q < 4; ++q) {
+            ws[q] = is6 ? bswap32(s[q]) : 0u;
+            wd[q] = is6 ? bswap32(d[q]) : 0u;
+        }
+        uint2 na = nt ? N[first] : empty, nb = nt ? N[first + 1u] : empty;
+        uint2 nc = nt ? N[first + 3u] : empty;
         for (;;) {
             const bool more = !(na.x & 16u) || !(nb.x & 16u) || !(nc.x & 16u);
             if (!__any(more)) break;
-            const uint32_t ia = child(na, addr_word(na, aw));
-            const uint32_t ib = child(nb, pv);
-            const uint32_t ic = child(nc, pr);
+            const uint32_t ia = child(na, addr_word(na, ws));
+            const uint32_t ib = child(nb, addr_word(nb, wd));
+            const uint32_t ic = child(nc, dp);
             const uint2 xa = N[ia], xb = N[ib], xc = N[ic];
             if (!(na.x & 16u)) na = xa;
             if (!(nb.x & 16u)) nb = xb;
@@ -905,7 +911,20 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
         }
         leaf_tests(na);
         leaf_tests(nb);
-        if (half == 0) leaf_tests(nc);
+        leaf_tests(nc);
+    }
+    {
+        uint2 na = nt ? N[first + 2u] : empty, nb = nt ? N[first + 4u] : empty;
+        for (;;) {
+            const bool more = !(na.x & 16u) || !(nb.x & 16u);
+            if (!__any(more)) break;
+            const uint32_t ia = child(na, sp), ib = child(nb, pr);
+            const uint2 xa = N[ia], xb = N[ib];
+            if (!(na.x & 16u)) na = xa;
+            if (!(nb.x & 16u)) nb = xb;
+        }
+        leaf_tests(na);
+        leaf_tests(nb);
     }
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
@@ -3462,14 +3481,15 @@ bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_
 // source port, destination port, protocol) whose range overlaps the fewest other rules of the
 // list (EffiCuts-style separation: a rule narrow only in its destination port is not copied into
 // every leaf of a tree that splits on addresses), one tree per field, each split on its own field's
-// words only (so that a walk compares one known key word per level: tree_match), every tree's
+// words (an address tree also on the ports and the protocol) only, so that a walk level selects
+// among few key words prepared before the walk (tree_match), every tree's
 // rules in list order; a field no rule is narrowest in gets an empty tree.  A key's first match
 // is the smallest of its first matches in the trees (the groups partition the list).  The
 // family's first rule that matches every key is no tree's, nor is any rule after it: it is the
 // answer when no tree has one (*def, its list position, else kNone).  roots: kTreeFields entries.
 constexpr int kTreeFields = 5;
 int tree_field(int d) { return d < 4 ? 0 : d < 8 ? 1 : d - 6; }
-constexpr uint32_t kTreeFieldDims[kTreeFields] = {0xFu, 0xF0u, 1u << 8, 1u << 9, 1u << 10};
+constexpr uint32_t kTreeFieldDims[kTreeFields] = {0x70Fu, 0x7F0u, 1u << 8, 1u << 9, 1u << 10};
 bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
                          size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots,
                          uint32_t* def) {

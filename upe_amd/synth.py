@@ -465,6 +465,22 @@ def _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, protos4, protos6,
     return rules_array(rules)
 
 
+def mixed_table(n_rules: int, seed: int) -> np.ndarray:
+    """A config-C-style table of n_rules random rules (_mixed_rules: prefixes /8-/32 and /32-/128
+    drawn from config C's host pools, ports exact or 0, 10 % version-agnostic): thousands of mask
+    signatures, so neither the tuple-space index nor an LDS copy applies (the 64k-rule parity test
+    and its timing probe)."""
+    rng = np.random.default_rng(seed)
+    n_hosts = 1000
+    v4_src = (0x0A000000 + rng.integers(0, 1 << 16, size=n_hosts) * 7).astype(np.uint64)
+    v4_dst = (0xAC100000 + rng.integers(0, 1 << 12, size=n_hosts)).astype(np.uint64)
+    v6_src = _v6_pool(rng, n_hosts)
+    v6_dst = _v6_pool(rng, n_hosts, prefix=bytes.fromhex("2001db80"))
+    ports = np.concatenate([np.array([53, 80, 443, 22, 123, 8080]),
+                            rng.integers(1024, 65536, size=200)])
+    return _mixed_rules(rng, n_rules, v4_src, v4_dst, v6_src, v6_dst, [17, 6, 1], [17, 6], ports)
+
+
 def config_c(n: int = 1 << 20, seed: int = 3, n_rules: int = 1024,
              v6_forwarding: bool = False) -> Workload:
     """BASELINE configs[2] as SURVEY.md §5 pins it (seed 3).  v6_forwarding: the same traffic
