@@ -15,6 +15,13 @@ import torch.multiprocessing as mp
 from upe_amd import shard, synth
 
 
+# B and the flow-derived C are the batches bench.py's strong-scaling leg splits into contiguous
+# shards (one batch over N ranks); seed-3-style C the round-1-4 IMIX draw
+WORKLOADS = {"B": lambda: synth.config_b(n=20000, seed=31),
+             "C": lambda: synth.config_c(n=12000, seed=32),
+             "CF": lambda: synth.config_c_flows(n=12000, seed=34)}
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -30,8 +37,7 @@ def _worker(rank, world, port, case, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        wl = {"B": lambda: synth.config_b(n=20000, seed=31),
-              "C": lambda: synth.config_c(n=12000, seed=32)}[case]()
+        wl = WORKLOADS[case]()
         sh = shard.shard_workload(wl, rank, world)
         r = oracle.run_restated(sh)
         counters = shard.sum_over_ranks([int(x) for x in r.counters[0].tolist()], dist)
@@ -45,7 +51,7 @@ def _worker(rank, world, port, case, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["B", "C"])
+@pytest.mark.parametrize("case", ["B", "C", "CF"])
 def test_two_rank_shards_sum_to_whole_batch(case):
     import oracle
 
@@ -61,8 +67,7 @@ def test_two_rank_shards_sum_to_whole_batch(case):
         assert p.exitcode == 0
     counters, stats, slowest, total = q.get(timeout=10)
 
-    wl = {"B": lambda: synth.config_b(n=20000, seed=31),
-          "C": lambda: synth.config_c(n=12000, seed=32)}[case]()
+    wl = WORKLOADS[case]()
     whole = oracle.run_restated(wl)
     assert total == wl.n
     assert slowest == 2.0
