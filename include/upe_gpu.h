@@ -406,16 +406,21 @@ typedef struct upe_worker_ops {
      * (the worker_t fields the stats thread reads, src/main.c:284-315: pkts_in, pkts_parsed,
      * pkts_matched, pkts_forwarded, pkts_dropped; the rest as upe_counters_t defines them) */
     void (*publish)(void *user, upe_gpu_ctx_t *ctx, const upe_counters_t *counters);
+    /* optional: the handles of a burst's forwarded frames after its tx_send_batch, in one call
+     * (else free_buf on each; src/worker.c:300-302 frees them one by one) */
+    void (*free_burst)(void *user, void *const *bufs, unsigned count);
 } upe_worker_ops_t;
 
 typedef struct {
     size_t batch;       /* most packets per GPU batch (0 = 65536) */
     unsigned burst;     /* most handles per pop (0 = 32, WORKER_BURST_SIZE; at most 64) */
-    /* NULL: each packet's first UPE_HDR_WINDOW bytes are copied into pinned staging and the batch
-     * goes through upe_gpu_process_host_emit (DMA round trip; records applied to the buffers on
-     * return).  Non-NULL: every buffer's frame lies at pool_base + a multiple of 16, inside
-     * memory registered with upe_gpu_host_register (e.g. the reference's pktbuf pool), and each
-     * batch is classified where it lies by upe_gpu_process_mapped (nothing copied). */
+    /* NULL: each packet's first UPE_HDR_WINDOW bytes are copied into pinned staging, shipped
+     * with the descriptors, classified in emit mode, and the verdicts and records come back
+     * (records applied to the buffers in the walk).  Non-NULL: every buffer's frame lies at
+     * pool_base + a multiple of 16, inside memory registered with upe_gpu_host_register (e.g.
+     * the reference's pktbuf pool), and each batch is classified where it lies by
+     * upe_gpu_process_mapped_emit (nothing copied; the records, written to pinned host memory,
+     * applied to the buffers in the walk). */
     uint8_t *pool_base;
     unsigned idle_ns;   /* sleep when the ring is empty and nothing is held (0 = 1000, as
                            src/worker.c:274-277) */

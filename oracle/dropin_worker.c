@@ -98,6 +98,10 @@ static int op_stop(void *u) { (void)u; return g_stop != 0; }
 static uint8_t *op_data(void *u, void *b) { (void)u; return ((pktbuf_t *)b)->data; }
 static size_t op_len(void *u, void *b) { (void)u; return ((pktbuf_t *)b)->len; }
 static void op_free(void *u, void *b) { pktbuf_free(GW(u)->w->pool, (pktbuf_t *)b); }
+static void op_free_burst(void *u, void *const *b, unsigned n) {
+    pktbuf_pool_t *pool = GW(u)->w->pool;
+    for (unsigned i = 0; i < n; i++) pktbuf_free(pool, (pktbuf_t *)b[i]);
+}
 static int op_tx_send(void *u, const uint8_t *f, size_t len) { return tx_send(GW(u)->w->tx, f, len); }
 static int op_tx_send_batch(void *u, const uint8_t *const *f, const size_t *lens, int count) {
     return tx_send_batch(GW(u)->w->tx, f, lens, count);
@@ -151,7 +155,7 @@ static void op_publish(void *u, upe_gpu_ctx_t *ctx, const upe_counters_t *c) {
 
 static const upe_worker_ops_t g_ops = {
     op_pop, op_stop, op_data, op_len, op_free, op_tx_send, op_tx_send_batch,
-    op_arp_update, op_ndp_update, op_load_neigh, op_poll, op_sync, op_publish,
+    op_arp_update, op_ndp_update, op_load_neigh, op_poll, op_sync, op_publish, op_free_burst,
 };
 
 /* The GPU worker thread: what worker_main is for a CPU worker. */

@@ -7,7 +7,7 @@ into legs at gaps longer than --gap-ms (the IMIX leg starts after its batch is g
 host, seconds later) and prints count / mean / min / max per leg, so that each leg's mean can
 be set beside the bench line's kernel_ms.
 
-Usage: python tools/kernel_legs.py <p_kernel_trace.csv> [--gap-ms 50] [--match upe_]
+Usage: python tools/kernel_legs.py <p_kernel_trace.csv | run_results.db> [--gap-ms 50] [--match upe_]
 """
 from __future__ import annotations
 
@@ -16,8 +16,20 @@ import csv
 import statistics
 
 
+def _rows(path: str, match: str):
+    """Kernel dispatches (name, start ns, end ns) from a kernel-trace CSV or, for rocprofv3's
+    SQLite output (`*_results.db`, ROCm 7), from its `kernels` view."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")
+                if match in n]
+    return [r for r in csv.DictReader(open(path)) if match in r["Kernel_Name"]]
+
+
 def legs(path: str, gap_ms: float, match: str):
-    rows = [r for r in csv.DictReader(open(path)) if match in r["Kernel_Name"]]
+    rows = _rows(path, match)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     by_name: dict[str, list[list[tuple[int, int]]]] = {}
     for r in rows:
@@ -35,11 +47,11 @@ def main() -> None:
     ap.add_argument("--gap-ms", type=float, default=50.0)
     ap.add_argument("--match", default="upe_")
     a = ap.parse_args()
-    print(f"{'kernel':70s} {'leg':>3s} {'calls':>6s} {'mean_us':>9s} {'min_us':>9s} {'max_us':>9s}")
+    print(f"{'kernel':100s} {'leg':>3s} {'calls':>6s} {'mean_us':>9s} {'min_us':>9s} {'max_us':>9s}")
     for name, segs in legs(a.trace, a.gap_ms, a.match).items():
         for i, seg in enumerate(segs):
             d = [(e - s) / 1e3 for s, e in seg]
-            print(f"{name[:70]:70s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
+            print(f"{name[:100]:100s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
                   f"{min(d):9.2f} {max(d):9.2f}")
 
 

@@ -152,7 +152,10 @@ static void flush_tx(loop_t *L) {
         if (sent > L->tx_count) sent = L->tx_count;
         L->c.pkts_forwarded += (uint64_t)sent;
         L->c.pkts_dropped += (uint64_t)(L->tx_count - sent);
-        for (int i = 0; i < L->tx_count; i++) L->ops->free_buf(L->user, L->tx_bufs[i]);
+        if (L->ops->free_burst)
+            L->ops->free_burst(L->user, L->tx_bufs, (unsigned)L->tx_count);
+        else
+            for (int i = 0; i < L->tx_count; i++) L->ops->free_buf(L->user, L->tx_bufs[i]);
         L->tx_count = 0;
     }
 }

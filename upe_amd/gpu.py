@@ -53,6 +53,7 @@ NDP_UPDATE_FN = ctypes.CFUNCTYPE(None, _VP, _U8P, _U8P)
 CTX_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP)
 POLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP)
 PUBLISH_FN = ctypes.CFUNCTYPE(None, _VP, _VP, _VP)
+FREE_BURST_FN = ctypes.CFUNCTYPE(None, _VP, _VP, ctypes.c_uint)
 
 
 class WorkerOps(ctypes.Structure):
@@ -61,7 +62,7 @@ class WorkerOps(ctypes.Structure):
                 ("free_buf", FREE_FN), ("tx_send", TX_SEND_FN), ("tx_send_batch", TX_BATCH_FN),
                 ("arp_update", ARP_UPDATE_FN), ("ndp_update", NDP_UPDATE_FN),
                 ("load_neigh", CTX_FN), ("poll", POLL_FN), ("sync", CTX_FN),
-                ("publish", PUBLISH_FN)]
+                ("publish", PUBLISH_FN), ("free_burst", FREE_BURST_FN)]
 
 
 class WorkerCfg(ctypes.Structure):
