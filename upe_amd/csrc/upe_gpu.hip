@@ -121,7 +121,7 @@ constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 #endif
 constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;
 constexpr uint32_t kNdpLdsSlots = UPE_NDP_LDS_SLOTS;
-constexpr size_t kLdsDynMax = 136 * 1024;
+constexpr size_t kLdsDynMax = 152 * 1024;   // 160 KB per CU less the static LDS (7 KB at most)
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kRingMax = 64;           // batches of a ring launch whose completion is stamped
@@ -826,6 +826,7 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
     const uint2 empty = make_uint2(16u, 0u);
+    const bool fam_lds = (a.fam4_lds || a.fam4 == 0u) && (a.fam6_lds || a.fam6 == 0u);
     // The leaf of one tree: its rules in list order until a match or a position >= best.
     auto leaf_tests = [&](const uint2 nd) {
         const uint32_t cnt = nd.x >> 5;
@@ -837,8 +838,32 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
                 if (p >= best) {
                     look = false;   // the lists ascend: nothing later in this leaf can win
                 } else {
-                    uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
                     const bool cov = (e >> 31) != 0u;
+                    if (fam_lds) {
+                        // both lists in LDS (the usual case): one address, the first two words
+                        // read for every lane, an IPv6 entry's other words in a masked block
+                        // that updates x in place (no zeroed registers to merge)
+                        const uint4* f = is6 ? l6 + kFamV6Stride * p : l4 + 2 * p;
+                        const uint4 e0 = f[0], e1 = f[1];
+                        uint32_t x6 = 0;
+                        if (is6) {   // (issued with the first two reads: no second round trip)
+                            const uint4 e2 = f[2], e3 = f[3], e4 = f[4];
+                            x6 = ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) |
+                                 ((s[3] ^ e2.z) & e3.y) | ((d[1] ^ e3.z) & e4.y) |
+                                 ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+                        }
+                        const uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                                           ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w) | x6;
+                        if (cov || x == 0u) {
+                            best = p;
+                            bact = e0.z;
+                            look = false;
+                        } else if (j + 1u >= cnt) {
+                            look = false;
+                        }
+                        continue;
+                    }
+                    uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
                     if (is6 && a.fam6_lds) {
                         const uint4* f = l6 + kFamV6Stride * p;
                         e0 = f[0];
