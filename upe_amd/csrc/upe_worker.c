@@ -97,7 +97,7 @@ typedef struct {
     int inplace;       /* mapped mode, UPE_WORKER_MAPPED_INPLACE=1 (diagnostic): the kernel
                           rewrites the frames in the pool instead of emitting records */
     int prof;
-    uint64_t t_wait, t_walk, t_launch, n_batches;
+    uint64_t t_wait, t_walk, t_launch, n_batches, t_flush;
 } loop_t;
 
 static uint64_t mono_ns(void) {
@@ -147,6 +147,7 @@ static void control_writes(loop_t *L, const uint8_t *d, size_t len, uint32_t v) 
 /* The TX flush of worker_main, src/worker.c:286-303. */
 static void flush_tx(loop_t *L) {
     if (L->tx_count > 0) {
+        const uint64_t t0 = L->prof ? mono_ns() : 0;
         int sent = L->ops->tx_send_batch(L->user, L->tx_frames, L->tx_lens, L->tx_count);
         if (sent < 0) sent = 0;
         if (sent > L->tx_count) sent = L->tx_count;
@@ -157,6 +158,21 @@ static void flush_tx(loop_t *L) {
         else
             for (int i = 0; i < L->tx_count; i++) L->ops->free_buf(L->user, L->tx_bufs[i]);
         L->tx_count = 0;
+        if (L->prof) L->t_flush += mono_ns() - t0;
+    }
+}
+
+/* upe_hdr_apply (upe_host.c) inlined into the walk: one record into its frame. */
+static inline void rec_apply(uint8_t *frame, const upe_hdr_rec_t *rec) {
+    const uint8_t fam = rec->b[15];
+    if (fam != 4 && fam != 6) return;
+    memcpy(frame, rec->b, 12);
+    if (fam == 4) {
+        frame[22] = rec->b[12];
+        frame[24] = rec->b[13];
+        frame[25] = rec->b[14];
+    } else {
+        frame[21] = rec->b[12];
     }
 }
 
@@ -213,13 +229,13 @@ static int walk(loop_t *L, int k) {
              * line is still in this core's cache from the gather (the kernel only reads the pool;
              * an answered ARP request it rewrote in place) */
             if ((i & 63u) == 0) rec = i;
-            if (code == UPE_V_FWD) upe_hdr_apply(d, &S->rec[rec++]);
+            if (code == UPE_V_FWD) rec_apply(d, &S->rec[rec++]);
         } else if (!L->pool) {
             /* window mode: the rewritten bytes into the caller's buffer (an answered ARP
              * request ends a cut batch, so nothing is queued behind it: a synchronous copy) */
             if ((i & 63u) == 0) rec = i;
             if (code == UPE_V_FWD) {
-                upe_hdr_apply(d, &S->rec[rec++]);
+                rec_apply(d, &S->rec[rec++]);
             } else if (v & UPE_VF_ARP_REPLY) {
                 const size_t c = len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT;
                 if (upe_gpu_memcpy_d2h(L->ctx, d, S->d_win + i * WIN, c, NULL) != 0 ||
@@ -467,10 +483,10 @@ fail:
 out:
     if (L.prof)
         fprintf(stderr, "upe_worker: %.3f s total, %llu batches (%.0f packets each): launch %.3f s, "
-                "GPU wait %.3f s, walk %.3f s, rest (pop + gather + idle) %.3f s\n",
+                "GPU wait %.3f s, walk %.3f s (of which TX flushes %.3f s), rest (pop + gather + idle) %.3f s\n",
                 (mono_ns() - t_start) * 1e-9, (unsigned long long)L.n_batches,
                 L.n_batches ? (double)L.c.pkts_in / (double)L.n_batches : 0.0, L.t_launch * 1e-9,
-                L.t_wait * 1e-9, L.t_walk * 1e-9,
+                L.t_wait * 1e-9, L.t_walk * 1e-9, L.t_flush * 1e-9,
                 (mono_ns() - t_start - L.t_launch - L.t_wait - L.t_walk) * 1e-9);
     if (counters) *counters = L.c;
     free(L.bq);
