@@ -2555,6 +2555,7 @@ struct upe_gpu_ctx {
     size_t rules_alloc = 0;
     uint32_t nrules = 0, nrules_pad = 0;
     unsigned long long* stats_idx = nullptr;   // [rules_alloc][2] totals per sorted index
+    bool host_tag = false;   // launches on behalf of a host-side loop (upe_gpu_tag_host)
     unsigned long long* hist_part = nullptr;   // [chunks][nrules_pad] dense group-by partials
     size_t hist_part_alloc = 0;
     void* gb = nullptr;                        // [gb_alloc] u32: group-by keys or u16 lengths
@@ -4017,6 +4018,15 @@ extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, s
     return load_rules_impl(c, rules, count, &fresh, rule_capacity);
 }
 
+// (not part of the ABI; upe_worker.c) tag this context's launches as a host-side loop's: they
+// run the host-path kernel instantiation (the same code), so that a profile of a process that
+// also classifies device-resident batches keeps the two kinds of launch apart
+extern "C" int upe_gpu_tag_host(upe_gpu_ctx_t* c, int on) {
+    if (!c) return fail("null context");
+    c->host_tag = on != 0;
+    return 0;
+}
+
 extern "C" int upe_gpu_rule_index_kind(upe_gpu_ctx_t* c) {
     if (!c) return fail("null context");
     return c->tss ? 1 : c->tree_ok ? 2 : 0;
@@ -4265,6 +4275,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
                  const RingReq* ring = nullptr, bool host = false) {
     if (!c) return fail("null context");
+    host = host || c->host_tag;
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
     if (n && (!d_frames || !d_desc || !d_verdict)) return fail("null batch buffer");
     if (((uintptr_t)d_frames & 15u) != 0) return fail("frames buffer must be 16-byte aligned");

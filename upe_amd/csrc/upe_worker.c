@@ -51,6 +51,7 @@
 int upe_gpu_set_last_error(const char *msg);
 int upe_gpu_mark(upe_gpu_ctx_t *ctx, int slot);
 int upe_gpu_mark_wait(upe_gpu_ctx_t *ctx, int slot);
+int upe_gpu_tag_host(upe_gpu_ctx_t *ctx, int on);
 
 #define WIN UPE_HDR_WINDOW
 #define NSLOT 2
@@ -405,6 +406,9 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
     L.bq_cap = NSLOT * (L.cap + L.burst) + 4;
     L.bq = malloc(L.bq_cap * sizeof(unsigned));
     int rc = 0;
+    /* (this loop's launches run the host-path kernel instantiation: profiles keep them apart from
+     * device-resident batches of the same process) */
+    (void)upe_gpu_tag_host(ctx, 1);
     if (!L.bq || alloc_slots(&L) != 0) {
         rc = upe_gpu_set_last_error("out of memory (worker loop buffers)");
         goto out;
@@ -489,6 +493,7 @@ out:
                 L.t_wait * 1e-9, L.t_walk * 1e-9, L.t_flush * 1e-9,
                 (mono_ns() - t_start - L.t_launch - L.t_wait - L.t_walk) * 1e-9);
     if (counters) *counters = L.c;
+    (void)upe_gpu_tag_host(ctx, 0);
     free(L.bq);
     free_slots(&L);
     return rc;
