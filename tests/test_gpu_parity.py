@@ -366,6 +366,25 @@ def test_lookback_far_first_hit(gpu_worker_factory, n, first_hit, emit):
                        "rule_stats": r.rule_stats, "l1": r.l1}, f"first_hit={first_hit}")
 
 
+@pytest.mark.parametrize("name,kind", [("B", 0), ("C3", 0), ("CF", 2), ("C6", 2), ("D", 1)])
+def test_default_rule_index(gpu_worker_factory, monkeypatch, name, kind):
+    """The index load_rules picks with no override: B's 8 rules and
+    seed-3 C (every list reaches its family catch-all within 64 entries) keep the scan, the
+    flow-derived C and C6 get the decision tree, D's 64k exact flows the tuple-space index."""
+    for k in ("UPE_GPU_TREE", "UPE_GPU_TSS"):
+        monkeypatch.delenv(k, raising=False)
+    wl = {"B": lambda: synth.config_b(n=4096), "C3": lambda: synth.config_c(n=4096),
+          "CF": lambda: synth.config_c_flows(n=4096),
+          "C6": lambda: synth.config_c(n=4096, v6_forwarding=True),
+          "D": lambda: synth.config_d(n=4096)}[name]()
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        assert w.rule_index_kind() == kind
+    finally:
+        w.close()
+
+
 @pytest.mark.parametrize("mode", ["scan", "tree", "tree-memory", "tss", "tss-unstaged"])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
                                   "config_cf_small", "config_d_small", "edge_inconsistent"])
