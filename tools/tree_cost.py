@@ -88,6 +88,11 @@ def main():
             walk += dep[:, :, g].max(axis=2).max(axis=1).mean()
             leaf_seq += stp[:, :, g].max(axis=1).sum(axis=1).mean()
             leaf_il += stp[:, :, g].max(axis=2).max(axis=1).mean()
+        # the kernel's grouping (tree_match): the deep trees (0 source, 1 destination address,
+        # 3 destination port) walked together, then the shallow ones (2 source port, 4 protocol)
+        deep = dep[:, :, [0, 1, 3]].max(axis=2).max(axis=1).mean()
+        shallow = dep[:, :, [2, 4]].max(axis=2).max(axis=1).mean()
+        print(f"{c}: kernel grouping: deep walk {deep:.1f} + shallow walk {shallow:.1f} iterations per wave")
         ilp = []
         for k in range(1, 6):
             it = sum(dep[:, :, g0:min(g0 + k, ntw)].max(axis=2).max(axis=1).mean()

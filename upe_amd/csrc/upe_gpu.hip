@@ -3612,6 +3612,29 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     return img.nodes.size() < (1u << 27);
 }
 
+// The tree of a table: the shortest leaves (at most 2, then 3, then kTreeBinth rules before a
+// split) whose image still leaves room in LDS for both family lists (list_bytes), a 1k-rule
+// rule_stats histogram and two 1k-slot neighbour indexes — the leaf tests read the lists from
+// LDS, and a list left in memory costs more than longer leaves (round 5: CF 73.8 / 71.0 / 87.6 us
+// at 4 / 3 / 2, whose image no longer fit; C6 83.7 / 79.2 / 76.6).  Tables whose lists cannot be
+// staged anyway get kTreeBinth.  forced: UPE_GPU_TREE_BINTH (diagnostic), 0 = choose.
+constexpr size_t kTreeLdsReserve = 56 * 1024;
+size_t tree_node_budget(size_t count);
+bool choose_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                 const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, size_t count,
+                 uint32_t forced, TreeImage& t) {
+    const size_t budget = tree_node_budget(count);
+    if (forced) return build_tree(v4, v6, l4, l6, forced, budget, t);
+    const size_t list_bytes = (2 * l4.size() + kFamV6Stride * l6.size()) * sizeof(uint4);
+    if (list_bytes + kTreeLdsReserve >= kLdsDynMax) return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
+    for (uint32_t b : {2u, 3u}) {
+        if (!build_tree(v4, v6, l4, l6, b, budget, t)) continue;
+        const size_t img = 8 * t.nodes.size() + 4 * t.leaves.size();
+        if (img + list_bytes + kTreeLdsReserve <= kLdsDynMax) return true;
+    }
+    return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
+}
+
 // Host walk of the image, bit for bit what tree_match does on the device: the list position of
 // the key's first match (kNone = none).  kv: the key words (kTreeDims comment).
 uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
@@ -3883,8 +3906,8 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
     const char* tf = getenv("UPE_GPU_TREE");
     if (!tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0')) {
         const char* bt = getenv("UPE_GPU_TREE_BINTH");
-        const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : kTreeBinth;
-        if (build_tree(v4, v6, l4, l6, binth, tree_node_budget(count), t)) {
+        const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : 0u;
+        if (choose_tree(v4, v6, l4, l6, count, binth, t)) {
             const size_t nw = 2 * t.nodes.size() + t.leaves.size();
             timg.assign((nw + 3) / 4, make_uint4(0, 0, 0, 0));
             memcpy(timg.data(), t.nodes.data(), t.nodes.size() * sizeof(uint2));
@@ -4068,9 +4091,9 @@ extern "C" int upe_tree_profile_host(const upe_rule_t* rules, size_t count,
     bool end4 = false, end6 = false;
     family_lists(rules, count, v4, v6, l4, l6, end4, end6);
     const char* bt = getenv("UPE_GPU_TREE_BINTH");
-    const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : kTreeBinth;
+    const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : 0u;
     TreeImage t;
-    const bool tree = build_tree(v4, v6, l4, l6, binth, tree_node_budget(count), t);
+    const bool tree = choose_tree(v4, v6, l4, l6, count, binth, t);
     if (info)
         *info = tree ? upe_rule_index_info_t{(uint64_t)t.nodes.size(), (uint64_t)t.leaves.size(),
                                              t.depth[0], t.depth[1], t.max_leaf,
