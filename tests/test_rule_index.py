@@ -152,12 +152,12 @@ def test_tree_equals_first_match_on_random_tables(seed, prefix_masks):
 
 def test_tree_shape_of_config_c():
     """Config C's forest fits the classify kernel's LDS beside its neighbour indexes and both family
-    lists (the leaf size is the shortest whose image leaves them room: ~37 KB); its five field
+    lists (the leaf size is the shortest whose image leaves them room: ~48 KB); its five field
     trees (split on their own field's words only) stay shallow, leaves short."""
     rs = synth.config_c_flows(n=16).rules_sorted
     _, info = gpu.rules_match_host(rs, np.zeros(0, FLOW_KEY_DTYPE))
     image = 8 * int(info["nodes"]) + 4 * int(info["leaf_entries"])
-    assert 0 < image < 40 * 1024, info
+    assert 0 < image < 56 * 1024, info
     assert info["depth4"] <= 16 and info["depth6"] <= 16 and info["max_leaf"] <= 16
     assert info["trees"] == 5 | 5 << 16
 

@@ -122,6 +122,9 @@ constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 constexpr uint32_t kArpLdsSlots = UPE_ARP_LDS_SLOTS;
 constexpr uint32_t kNdpLdsSlots = UPE_NDP_LDS_SLOTS;
 constexpr size_t kLdsDynMax = 152 * 1024;   // 160 KB per CU less the static LDS (7 KB at most)
+// kernels for linear tables past kSmallRules (family lists, whole-table scan, decision tree) keep
+// no small-table copy in static LDS (~1 KB static): 158 KB for their dynamic LDS
+constexpr size_t kLdsDynMaxLarge = 158 * 1024;
 constexpr int kSmallRules = 64;        // up to here rule_stats go through replicated accumulators
 constexpr int kReps = 32;              // replicas of the per-batch accumulators
 constexpr int kRingMax = 64;           // batches of a ring launch whose completion is stamped
@@ -1486,8 +1489,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ uint32_t s_tot[C_N + 3];   // the workgroup's counters; first f4 / f6 / ctrl (min)
     __shared__ uint32_t s_wm[kWaves][2];  // per wave: its last table hit per family (index + 1)
     __shared__ uint32_t s_pay[kWaves][kPayWords];   // ... and that hit's (ip, MAC)
-    __shared__ u32x8 s_rv4[kTssMode ? 1 : kSmallRules];    // small tables: RuleV4 / RuleV6 words
-    __shared__ u32x16 s_rv6[kTssMode ? 1 : kSmallRules];
+    __shared__ u32x8 s_rv4[kTssMode || kScan ? 1 : kSmallRules];   // small tables: RuleV4 / RuleV6
+    __shared__ u32x16 s_rv6[kTssMode || kScan ? 1 : kSmallRules];  // words (only kScan 0 has them)
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
     __shared__ uint32_t s_bdone[kRing ? kRingMax : 1];   // ring: the workgroup's chunks done per batch
 
@@ -2897,7 +2900,8 @@ void launch_classify(int var, uint32_t grid, size_t lds, hipStream_t s, const Ar
         for (int v = 0; v < kVarCount; ++v)
             if (classify_fn(v))
                 (void)hipFuncSetAttribute(classify_fn(v), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)kLdsDynMax);
+                                          (int)((v & VAR_SCAN) && !(v & VAR_TSS) ? kLdsDynMaxLarge
+                                                                                 : kLdsDynMax));
     Args arg = a;
     void* args[] = {&arg};
     (void)hipLaunchKernel(classify_fn(var), dim3(grid), dim3(kBlock), args, lds, s);
@@ -3626,11 +3630,11 @@ bool choose_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     const size_t budget = tree_node_budget(count);
     if (forced) return build_tree(v4, v6, l4, l6, forced, budget, t);
     const size_t list_bytes = (2 * l4.size() + kFamV6Stride * l6.size()) * sizeof(uint4);
-    if (list_bytes + kTreeLdsReserve >= kLdsDynMax) return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
+    if (list_bytes + kTreeLdsReserve >= kLdsDynMaxLarge) return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
     for (uint32_t b : {2u, 3u}) {
         if (!build_tree(v4, v6, l4, l6, b, budget, t)) continue;
         const size_t img = 8 * t.nodes.size() + 4 * t.leaves.size();
-        if (img + list_bytes + kTreeLdsReserve <= kLdsDynMax) return true;
+        if (img + list_bytes + kTreeLdsReserve <= kLdsDynMaxLarge) return true;
     }
     return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
 }
@@ -4396,45 +4400,46 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
         a.gb = c->gb;
     }
     const size_t hist = lds_stats ? 2 * (size_t)c->nrules_pad * sizeof(uint32_t) : 0;
+    // large linear tables: the decision tree (when built), else family lists, unless a family's
+    // list is a single catch-all (then the split gains that family nothing and measured slower
+    // for the other)
+    const int scan = c->tss || c->nrules_pad <= (uint32_t)kSmallRules ? 0
+                   : c->tree_ok ? 3 : c->fam_all ? 2 : 1;
+    const size_t lds_max = scan ? kLdsDynMaxLarge : kLdsDynMax;
     // stage the ARP index in LDS when it is small (the nrules_pad multiple of 4 keeps the slot
     // array 16-byte aligned after the bins)
     const uint32_t arp_slots = c->arp_bits ? (1u << c->arp_bits) : 0u;
     const uint32_t ndp_slots = c->ndp_bits ? (1u << c->ndp_bits) : 0u;
     size_t lds = hist;
     a.arp_lds = a.ndp_lds = 0u;
-    if (arp_slots && arp_slots <= kArpLdsSlots && lds + arp_slots * sizeof(uint4) <= kLdsDynMax) {
+    if (arp_slots && arp_slots <= kArpLdsSlots && lds + arp_slots * sizeof(uint4) <= lds_max) {
         a.arp_lds = arp_slots;
         lds += arp_slots * sizeof(uint4);
     }
-    if (ndp_slots && ndp_slots <= kNdpLdsSlots && lds + 2 * ndp_slots * sizeof(uint4) <= kLdsDynMax) {
+    if (ndp_slots && ndp_slots <= kNdpLdsSlots && lds + 2 * ndp_slots * sizeof(uint4) <= lds_max) {
         a.ndp_lds = ndp_slots;
         lds += 2 * ndp_slots * sizeof(uint4);
     }
     a.fp_lds = 0u;
-    if (c->tss && c->nfs && lds + c->nfs * sizeof(uint4) <= kLdsDynMax) {
+    if (c->tss && c->nfs && lds + c->nfs * sizeof(uint4) <= lds_max) {
         a.fp_lds = c->nfs;
         lds += c->nfs * sizeof(uint4);
     }
-    // large linear tables: the decision tree (when built), else family lists, unless a family's
-    // list is a single catch-all (then the split gains that family nothing and measured slower
-    // for the other)
-    const int scan = c->tss || c->nrules_pad <= (uint32_t)kSmallRules ? 0
-                   : c->tree_ok ? 3 : c->fam_all ? 2 : 1;
     // the tree's image in LDS first (every lane reads a node per level), then the IPv6 list
     a.tree_lds = 0u;
-    if (scan == 3 && c->tree_stage && lds + c->tree_words * sizeof(uint4) <= kLdsDynMax) {
+    if (scan == 3 && c->tree_stage && lds + c->tree_words * sizeof(uint4) <= lds_max) {
         a.tree_lds = c->tree_words;
         lds += c->tree_words * sizeof(uint4);
     }
     a.fam6_lds = 0u;
     if (kFamLds && !c->tss && (scan == 3 || !c->fam_all) && c->fam6 &&
-        lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= kLdsDynMax) {
+        lds + kFamV6Stride * c->fam6 * sizeof(uint4) <= lds_max) {
         a.fam6_lds = 1u;
         lds += kFamV6Stride * c->fam6 * sizeof(uint4);
     }
     // the tree kernels' leaf tests read the IPv4 list's rule words too: from LDS when it fits
     a.fam4_lds = 0u;
-    if (scan == 3 && c->tree_stage && c->fam4 && lds + 2 * c->fam4 * sizeof(uint4) <= kLdsDynMax) {
+    if (scan == 3 && c->tree_stage && c->fam4 && lds + 2 * c->fam4 * sizeof(uint4) <= lds_max) {
         a.fam4_lds = 1u;
         lds += 2 * c->fam4 * sizeof(uint4);
     }
