@@ -3616,7 +3616,7 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     return img.nodes.size() < (1u << 27);
 }
 
-// The tree of a table: the shortest leaves (at most 2, then 3, then kTreeBinth rules before a
+// The tree of a table: the shortest leaves (at most 1, 2, 3, then kTreeBinth rules before a
 // split) whose image still leaves room in LDS for both family lists (list_bytes), a 1k-rule
 // rule_stats histogram and two 1k-slot neighbour indexes — the leaf tests read the lists from
 // LDS, and a list left in memory costs more than longer leaves (round 5: CF 73.8 / 71.0 / 87.6 us
@@ -3631,7 +3631,7 @@ bool choose_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     if (forced) return build_tree(v4, v6, l4, l6, forced, budget, t);
     const size_t list_bytes = (2 * l4.size() + kFamV6Stride * l6.size()) * sizeof(uint4);
     if (list_bytes + kTreeLdsReserve >= kLdsDynMaxLarge) return build_tree(v4, v6, l4, l6, kTreeBinth, budget, t);
-    for (uint32_t b : {2u, 3u}) {
+    for (uint32_t b : {1u, 2u, 3u}) {
         if (!build_tree(v4, v6, l4, l6, b, budget, t)) continue;
         const size_t img = 8 * t.nodes.size() + 4 * t.leaves.size();
         if (img + list_bytes + kTreeLdsReserve <= kLdsDynMaxLarge) return true;
