@@ -6,7 +6,7 @@ Per 64-packet wave (the kernel's chunk): the walk's loop iterations (ILP groups 
 as long as the wave's deepest walk in it) and the leaf loop's iterations, tree by tree (as built)
 or interleaved over a group's trees, from upe_tree_profile_host (the host walk of the same image:
 levels walked and leaf entries read per key and tree).  Environment knobs of the builder
-(UPE_GPU_TREE_DIMS, UPE_GPU_TREE_GROUP, UPE_GPU_TREE_BINTH) apply."""
+(UPE_GPU_TREE_BINTH) applies."""
 from __future__ import annotations
 
 import argparse

@@ -4,7 +4,7 @@
 
 cases: CF (config C, flow-derived rules), C3 (seed-3 config C), C6 (C with IPv6 forwarded),
 each as <case>:<flavour> with flavour tree (decision tree, image staged in LDS), treemem (the
-tree read from memory), treeword (one tree per key word instead of per field), scan (UPE_GPU_TREE=0: family lists /
+tree read from memory), scan (UPE_GPU_TREE=0: family lists /
 whole-table scan).  Emit mode,
 batches queued from native code (upe_gpu_process_batches_emit) over 8 distinct copies; HIP-event
 kernel time per launch (upe_gpu_timing_*), plus a check of the verdicts against the previous
@@ -27,8 +27,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tree_probe.jsonl"))
-    ap.add_argument("cases", nargs="*", default=["CF:tree", "CF:treeword", "CF:treemem", "CF:scan",
-                                                  "C6:tree", "C6:treeword", "C6:scan", "C3:tree",
+    ap.add_argument("cases", nargs="*", default=["CF:tree", "CF:treemem", "CF:scan",
+                                                  "C6:tree", "C6:scan", "C3:tree",
                                                   "C3:scan"])
     args = ap.parse_args()
     import torch
@@ -58,7 +58,6 @@ def main() -> None:
         wl = cache[name]
         os.environ["UPE_GPU_TREE"] = "0" if flavour == "scan" else "1"
         os.environ["UPE_GPU_TREE_LDS"] = "0" if flavour == "treemem" else "1"
-        os.environ["UPE_GPU_TREE_GROUP"] = "word" if flavour == "treeword" else "field"
         w = gpu.GpuWorker(0, wl.capacity)
         w.configure(wl)
         n = wl.n
