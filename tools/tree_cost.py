@@ -99,6 +99,10 @@ def main():
                      for g0 in range(0, ntw, k))
             ilp.append(f"ilp{k}: {it:.1f} it / {it * k:.1f} slots")
         print(f"{c}: walk " + ", ".join(ilp))
+        for t in range(2 * 5 if ntw == 5 else 16):
+            if stp[:, :, t].any() or dep[:, :, t].any():
+                print(f"{c}: tree slot {t}: wave walk {dep[:, :, t].max(axis=1).mean():.1f}, wave leaf "
+                      f"{stp[:, :, t].max(axis=1).mean():.1f}, lane leaf {stp[:, :, t].mean():.2f}")
         lane_walk = dep.sum(axis=2).mean()
         lane_steps = stp.sum(axis=2).mean()
         print(f"{c}: index {info[0].tolist()} trees/family {ntw}; per wave: walk iterations "

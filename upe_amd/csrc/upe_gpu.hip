@@ -824,7 +824,7 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint2* N = kLdsTree ? lnodes : a.tree;
     const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
     const uint2 dir = N[0];
-    const uint32_t nt = active ? (is6 ? dir.y : dir.x) : 0u, first = 2u + (is6 ? dir.x : 0u);
+    const uint32_t nt = active ? (is6 ? dir.y & 0xFFFFu : dir.x) : 0u, first = 2u + (is6 ? dir.x : 0u);
     const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
@@ -916,13 +916,13 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     {
         // the deep trees together (source and destination address, destination port), then the
         // shallow ones (source port, protocol: few distinct values)
+        // (IPv6 words big-endian where the image says so: tree_swap6)
+        const uint32_t sw6 = is6 ? dir.y >> 16 : 0u;
         uint32_t ws[4], wd[4];
-        ws[0] = is6 ? bswap32(s[0]) : s[0];
-        wd[0] = is6 ? bswap32(d[0]) : d[0];
 #pragma unroll
-        for (int q = 1; q < 4; ++q) {
-            ws[q] = is6 ? bswap32(s[q]) : 0u;
-            wd[q] = is6 ? bswap32(d[q]) : 0u;
+        for (int q = 0; q < 4; ++q) {
+            ws[q] = (sw6 >> q & 1u) ? bswap32(s[q]) : (is6 || q == 0) ? s[q] : 0u;
+            wd[q] = (sw6 >> (4 + q) & 1u) ? bswap32(d[q]) : (is6 || q == 0) ? d[q] : 0u;
         }
         uint2 na = nt ? N[first] : empty, nb = nt ? N[first + 1u] : empty;
         uint2 nc = nt ? N[first + 3u] : empty;
@@ -3350,21 +3350,24 @@ struct TreeRule {
 constexpr uint32_t kTreeWidth[kTreeDims] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                             0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                             0xFFFFu, 0xFFFFu, 0xFFu};
-// A family list entry (RuleV4 words, plus the IPv6 words for family 6) as key-word ranges.  IPv6
-// address words are compared big-endian (a prefix is then a range); IPv4 word 0 is host order
-// already (src/parser.c:40-41) and its other address words are 0 in the key.
-TreeRule tree_rule(int F, const RuleV4& r, const RuleV6* q) {
+// A family list entry (RuleV4 words, plus the IPv6 words for family 6) as key-word ranges.  IPv4
+// word 0 is host order already (src/parser.c:40-41) and its other address words are 0 in the key.
+// An IPv6 address word is compared big-endian (a prefix is then a range) when bit j (source word
+// j) or 4 + j (destination word j) of swap6 is set, else as loaded: a version-agnostic rule's
+// IPv4 prefix (host order, src/rule_config.c:60-66) is a range only that way (tree_swap6).
+uint32_t word_of(uint32_t v, uint32_t swap6, int j) { return (swap6 >> j & 1u) ? bswap32(v) : v; }
+TreeRule tree_rule(int F, const RuleV4& r, const RuleV6* q, uint32_t swap6 = 0xFFu) {
     TreeRule t;
     uint32_t x[kTreeDims] = {}, m[kTreeDims] = {};
     if (F == 4) {
         x[0] = r.s0; m[0] = r.sm0;
         x[4] = r.d0; m[4] = r.dm0;
     } else {
-        x[0] = bswap32(r.s0); m[0] = bswap32(r.sm0);
-        x[4] = bswap32(r.d0); m[4] = bswap32(r.dm0);
-        for (int j = 1; j < 4; ++j) {
-            x[j] = bswap32(q->s[j - 1]); m[j] = bswap32(q->sm[j - 1]);
-            x[4 + j] = bswap32(q->d[j - 1]); m[4 + j] = bswap32(q->dm[j - 1]);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t xs = j ? q->s[j - 1] : r.s0, ms = j ? q->sm[j - 1] : r.sm0;
+            const uint32_t xd = j ? q->d[j - 1] : r.d0, md = j ? q->dm[j - 1] : r.dm0;
+            x[j] = word_of(xs, swap6, j); m[j] = word_of(ms, swap6, j);
+            x[4 + j] = word_of(xd, swap6, 4 + j); m[4 + j] = word_of(md, swap6, 4 + j);
         }
     }
     x[8] = r.x0 >> 16; m[8] = r.m0 >> 16;
@@ -3386,7 +3389,28 @@ struct TreeImage {
     uint32_t trees[2] = {0, 0};      // trees per family
     uint32_t depth[2] = {0, 0};      // deepest leaf per family
     uint32_t max_leaf = 0;           // longest leaf list
+    uint32_t swap6 = 0xFFu;          // IPv6 address words compared big-endian (tree_rule)
 };
+
+// The byte order of each IPv6 address word under which more of the family's rules are ranges
+// (exact): big-endian for IPv6 prefixes, as loaded for version-agnostic IPv4 prefixes in the
+// IPv6 list (config C's 10 %); ties big-endian.
+uint32_t tree_swap6(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                    const std::vector<uint32_t>& l6) {
+    auto exact = [](uint32_t m) { const uint32_t inv = ~m; return (inv & (inv + 1u)) == 0; };
+    uint32_t swap6 = 0;
+    for (int w = 0; w < 8; ++w) {
+        const int j = w & 3;
+        long votes = 0;
+        for (uint32_t i : l6) {
+            const uint32_t m = w < 4 ? (j ? v6[i].sm[j - 1] : v4[i].sm0)
+                                     : (j ? v6[i].dm[j - 1] : v4[i].dm0);
+            votes += (long)exact(bswap32(m)) - (long)exact(m);
+        }
+        if (votes >= 0) swap6 |= 1u << w;
+    }
+    return swap6;
+}
 
 // HyperSplit-style build of one family's tree into img (breadth first, so the top levels are
 // contiguous).  rules: the family list's entries in list order.  Returns false when the node
@@ -3596,13 +3620,14 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     for (uint32_t i : l4) R.push_back(tree_rule(4, v4[i], nullptr));
     if (!build_forest_family(R, 0, binth, node_budget, body, r4, &def4)) return false;
     R.clear();
-    for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i]));
+    const uint32_t swap6 = tree_swap6(v4, v6, l6);
+    for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i], swap6));
     if (!build_forest_family(R, 1, binth, node_budget, body, r6, &def6)) return false;
     const uint32_t dir = 2u + (uint32_t)(r4.size() + r6.size());
     auto shift = [&](uint2 nd) {   // inner nodes' child indexes move by the directory's size
         return (nd.x & 16u) ? nd : make_uint2((nd.x & 15u) | (((nd.x >> 5) + dir) << 5), nd.y);
     };
-    img.nodes.push_back(make_uint2((uint32_t)r4.size(), (uint32_t)r6.size()));
+    img.nodes.push_back(make_uint2((uint32_t)r4.size(), (uint32_t)r6.size() | swap6 << 16));
     img.nodes.push_back(make_uint2(def4, def6));
     for (uint32_t r : r4) img.nodes.push_back(shift(body.nodes[r]));
     for (uint32_t r : r6) img.nodes.push_back(shift(body.nodes[r]));
@@ -3613,6 +3638,7 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     img.max_leaf = body.max_leaf;
     img.trees[0] = (uint32_t)r4.size();
     img.trees[1] = (uint32_t)r6.size();
+    img.swap6 = swap6;
     return img.nodes.size() < (1u << 27);
 }
 
@@ -3647,7 +3673,7 @@ uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
                         const uint32_t d[4], uint8_t* prof_depth = nullptr,
                         uint8_t* prof_steps = nullptr) {
     const uint2 dir = img.nodes[0], dflt = img.nodes[1];
-    const uint32_t nt = is6 ? dir.y : dir.x, first = 2u + (is6 ? dir.x : 0u);
+    const uint32_t nt = is6 ? dir.y & 0xFFFFu : dir.x, first = 2u + (is6 ? dir.x : 0u);
     uint32_t best = kNone;
     for (uint32_t t = 0; t < nt; ++t) {
         uint2 nd = img.nodes[first + t];
@@ -4120,8 +4146,8 @@ extern "C" int upe_tree_profile_host(const upe_rule_t* rules, size_t count,
         }
         if (is6) {
             for (int j = 0; j < 4; ++j) {
-                kv[j] = bswap32(sw[j]);
-                kv[4 + j] = bswap32(dw[j]);
+                kv[j] = word_of(sw[j], t.swap6, j);
+                kv[4 + j] = word_of(dw[j], t.swap6, 4 + j);
             }
         } else {
             kv[0] = sw[0];
