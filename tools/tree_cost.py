@@ -62,7 +62,8 @@ def main():
     lib = gpu.LIB
     lib.upe_tree_profile_host.restype = ctypes.c_int
     makers = {"CF": lambda: synth.config_c_flows(n=args.n), "C3": lambda: synth.config_c(n=args.n),
-              "C6": lambda: synth.config_c(n=args.n, v6_forwarding=True)}
+              "C6": lambda: synth.config_c(n=args.n, v6_forwarding=True),
+              "F16k": lambda: synth.config_c_flows(seed=62, n_rules=1 << 14, max_cover=2.0 ** -18)}
     P = ctypes.c_void_p
     for c in args.cases:
         wl = makers[c]()

@@ -297,16 +297,22 @@ constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 // Key words: 0-3 source address, 4-7 destination address (IPv6: the wire bytes as big-endian
 // words, so that a prefix is a range; IPv4: word 0 host order as parse_flow_key stores it, the
 // other words 0), 8 source port, 9 destination port, 10 protocol.
-//   node (uint2): inner {dim | child << 5, threshold}: key word < threshold -> child, else child+1
-//                 leaf  {16 | count << 5, first entry}
+// The binary tree is built (build_tree_family), then packed two levels to a node, so that a walk
+// step resolves two levels with one 16-byte load (the walk is a chain of dependent LDS loads):
+//   node (uint4): {x, y, z, w}: x = dim P | dim L << 4 | dim R << 8 | P leaf << 12 | L leaf << 13 |
+//                 R leaf << 14 | base << 15; y = P's threshold (P leaf: its leaf word); z / w =
+//                 the threshold of P's left / right child L / R, or its leaf word.  A key word <
+//                 threshold goes left.  L's children are nodes base, base + 1; R's follow them
+//                 (base, base + 1 when L is a leaf).
+//   leaf word: count << 21 | first entry
 //   leaf entry (u32): list position | 0x80000000 when the rule matches every key of the leaf
 // Each family's rules are split into groups by the key field on which each is narrowest, one
 // tree per group (a rule narrow only in a port is then not copied into every leaf of a tree cut on
 // addresses); a key's first match is the smallest of its first matches over its family's trees,
 // else the family's rule that matches every key (build_forest_family).
-// Image: a directory (node 0 = {IPv4 trees, IPv6 trees}, node 1 = {IPv4, IPv6 default answer},
-// then a copy of each tree's root, IPv4 first), the nodes, then the leaf entries; staged in LDS
-// when it fits beside the launch's other LDS data.
+// Image: a directory (node 0 = {IPv4 trees, IPv6 trees | byte orders << 16, IPv4 default answer,
+// IPv6 default answer}), each tree's root node (IPv4 first), the other nodes, then the leaf
+// entries; staged in LDS when it fits beside the launch's other LDS data.
 constexpr int kTreeDims = 11;
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
 constexpr size_t kTreeMinReach = 64;   // (load_rules_impl: tree or scan)
@@ -812,9 +818,10 @@ __device__ __forceinline__ uint32_t scan_fam(const Args& a, bool done, bool is6,
 // address tree also on the ports and the protocol), so each level compares one of a few key words
 // prepared before the walk (an address tree: one of its field's four words or a port word, by
 // the node's dimension bits).  Walks are per lane (divergent loads: LDS when
-// the image is staged, else memory), the deep trees together (source and destination address,
-// destination port), then the shallow ones (source port, protocol), node loads in flight together;
-// the wave iterates as long as its deepest walk and its longest leaf, tree by tree.  Returns the
+// the image is staged, else memory), two levels per 16-byte node load, the deep trees together
+// (source and destination address, destination port), then the shallow ones (source port,
+// protocol), node loads in flight together; the wave iterates as long as its deepest walk and
+// its longest leaf, tree by tree.  Returns the
 // lane's FamTable index-array entry, as scan_fam.
 template <bool kLdsTree>
 __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool is6, uint32_t k0,
@@ -824,19 +831,18 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint2* N = kLdsTree ? lnodes : a.tree;
     const uint32_t* E = reinterpret_cast<const uint32_t*>(N) + a.tree_loff;
     const uint2 dir = N[0];
-    const uint32_t nt = active ? (is6 ? dir.y & 0xFFFFu : dir.x) : 0u, first = 2u + (is6 ? dir.x : 0u);
+    const uint32_t nt = active ? (is6 ? dir.y & 0xFFFFu : dir.x) : 0u, first = 1u + (is6 ? dir.x : 0u);
     const uint32_t sp = k0 >> 16, dp = k1, pr = (k0 >> 8) & 0xFFu;
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
-    const uint2 empty = make_uint2(16u, 0u);
     const bool fam_lds = (a.fam4_lds || a.fam4 == 0u) && (a.fam6_lds || a.fam6 == 0u);
     // The leaf of one tree: its rules in list order until a match or a position >= best.
-    auto leaf_tests = [&](const uint2 nd) {
-        const uint32_t cnt = nd.x >> 5;
+    auto leaf_tests = [&](const uint32_t lw) {
+        const uint32_t cnt = lw >> 21, off = lw & 0x1FFFFFu;
         bool look = cnt != 0u;
         for (uint32_t j = 0; __any(look); ++j) {
             if (look) {
-                const uint32_t e = E[nd.y + j];
+                const uint32_t e = E[off + j];
                 const uint32_t p = e & 0x7FFFFFFFu;
                 if (p >= best) {
                     look = false;   // the lists ascend: nothing later in this leaf can win
@@ -900,23 +906,38 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             }
         }
     };
-    // one level of a tree: the child a key word picks (0 = stay: the directory word, a broadcast)
-    auto child = [](const uint2 nd, uint32_t v) -> uint32_t {
-        return (nd.x & 16u) ? 0u : (nd.x >> 5) + (v >= nd.y ? 1u : 0u);
-    };
-    // an address tree's key word for a node: one of its field's words (big-endian for IPv6, so
-    // that a prefix is a range; IPv4's host-order word 0 and zeros), or a port or the protocol
-    // (dimensions 8-10); bit selects keep them in registers
-    auto addr_word = [&](const uint2 nd, const uint32_t (&w)[4]) -> uint32_t {
-        const uint32_t m1 = 0u - (nd.x & 1u), m2 = 0u - ((nd.x >> 1) & 1u);
-        const uint32_t m8 = 0u - ((nd.x >> 3) & 1u);
+    // an address tree's key word for a dimension: one of its field's words (big-endian for IPv6
+    // where the image says so, so that a prefix is a range; IPv4's host-order word 0 and zeros),
+    // or a port or the protocol (dimensions 8-10); bit selects keep them in registers
+    auto addr_word = [&](const uint32_t dm, const uint32_t (&w)[4]) -> uint32_t {
+        const uint32_t m1 = 0u - (dm & 1u), m2 = 0u - ((dm >> 1) & 1u);
+        const uint32_t m8 = 0u - ((dm >> 3) & 1u);
         const uint32_t aw = vsel(m2, vsel(m1, w[3], w[2]), vsel(m1, w[1], w[0]));
         return vsel(m8, vsel(m2, pr, vsel(m1, dp, sp)), aw);
     };
+    // one walk step (two levels, Args::tree comment): the next node, or the leaf (live = false)
+    auto step = [](const uint4 q, uint32_t& idx, uint32_t& leaf, bool& live, auto key) {
+        const bool c1 = key(q.x & 15u) >= q.y;
+        const uint32_t lleaf = (q.x >> 13) & 1u;
+        const bool cl = c1 ? ((q.x >> 14) & 1u) != 0u : lleaf != 0u;
+        const uint32_t ct = c1 ? q.w : q.z;
+        const uint32_t c2 = key(c1 ? (q.x >> 8) & 15u : (q.x >> 4) & 15u) >= ct ? 1u : 0u;
+        if (live) {
+            if (q.x & 0x1000u) {
+                leaf = q.y;
+                live = false;
+            } else if (cl) {
+                leaf = ct;
+                live = false;
+            } else {
+                idx = (q.x >> 15) + ((c1 && !lleaf) ? 2u : 0u) + c2;
+            }
+        }
+    };
+    const uint4* S = reinterpret_cast<const uint4*>(N);
     {
         // the deep trees together (source and destination address, destination port), then the
-        // shallow ones (source port, protocol: few distinct values)
-        // (IPv6 words big-endian where the image says so: tree_swap6)
+        // shallow ones (source port, protocol: few distinct values); node loads in flight together
         const uint32_t sw6 = is6 ? dir.y >> 16 : 0u;
         uint32_t ws[4], wd[4];
 #pragma unroll
@@ -924,35 +945,28 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             ws[q] = (sw6 >> q & 1u) ? bswap32(s[q]) : (is6 || q == 0) ? s[q] : 0u;
             wd[q] = (sw6 >> (4 + q) & 1u) ? bswap32(d[q]) : (is6 || q == 0) ? d[q] : 0u;
         }
-        uint2 na = nt ? N[first] : empty, nb = nt ? N[first + 1u] : empty;
-        uint2 nc = nt ? N[first + 3u] : empty;
-        for (;;) {
-            const bool more = !(na.x & 16u) || !(nb.x & 16u) || !(nc.x & 16u);
-            if (!__any(more)) break;
-            const uint32_t ia = child(na, addr_word(na, ws));
-            const uint32_t ib = child(nb, addr_word(nb, wd));
-            const uint32_t ic = child(nc, dp);
-            const uint2 xa = N[ia], xb = N[ib], xc = N[ic];
-            if (!(na.x & 16u)) na = xa;
-            if (!(nb.x & 16u)) nb = xb;
-            if (!(nc.x & 16u)) nc = xc;
+        uint32_t ia = first, ib = first + 1u, ic = first + 3u, la = 0, lb = 0, lc = 0;
+        bool va = nt != 0u, vb = va, vc = va;
+        while (__any(va || vb || vc)) {
+            const uint4 qa = S[ia], qb = S[ib], qc = S[ic];
+            step(qa, ia, la, va, [&](uint32_t dm) { return addr_word(dm, ws); });
+            step(qb, ib, lb, vb, [&](uint32_t dm) { return addr_word(dm, wd); });
+            step(qc, ic, lc, vc, [&](uint32_t) { return dp; });
         }
-        leaf_tests(na);
-        leaf_tests(nb);
-        leaf_tests(nc);
+        leaf_tests(la);
+        leaf_tests(lb);
+        leaf_tests(lc);
     }
     {
-        uint2 na = nt ? N[first + 2u] : empty, nb = nt ? N[first + 4u] : empty;
-        for (;;) {
-            const bool more = !(na.x & 16u) || !(nb.x & 16u);
-            if (!__any(more)) break;
-            const uint32_t ia = child(na, sp), ib = child(nb, pr);
-            const uint2 xa = N[ia], xb = N[ib];
-            if (!(na.x & 16u)) na = xa;
-            if (!(nb.x & 16u)) nb = xb;
+        uint32_t ia = first + 2u, ib = first + 4u, la = 0, lb = 0;
+        bool va = nt != 0u, vb = va;
+        while (__any(va || vb)) {
+            const uint4 qa = S[ia], qb = S[ib];
+            step(qa, ia, la, va, [&](uint32_t) { return sp; });
+            step(qb, ib, lb, vb, [&](uint32_t) { return pr; });
         }
-        leaf_tests(na);
-        leaf_tests(nb);
+        leaf_tests(la);
+        leaf_tests(lb);
     }
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
@@ -3546,8 +3560,9 @@ int tree_field(int d) { return d < 4 ? 0 : d < 8 ? 1 : d - 6; }
 constexpr uint32_t kTreeFieldDims[kTreeFields] = {0x70Fu, 0x7F0u, 1u << 8, 1u << 9, 1u << 10};
 bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
                          size_t node_budget, TreeImage& img, std::vector<uint32_t>& roots,
-                         uint32_t* def) {
+                         uint32_t* def, const std::vector<TreeRule>* RG = nullptr) {
     const size_t n = R.size();
+    const std::vector<TreeRule>& G = RG ? *RG : R;
     roots.clear();
     *def = kNone;
     std::vector<int> grp(n, -1);
@@ -3555,15 +3570,15 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
     std::vector<uint32_t> los(n), his(n);
     for (int d = 0; d < kTreeDims && n > 0; ++d) {
         for (size_t i = 0; i < n; ++i) {
-            los[i] = R[i].lo[d];
-            his[i] = R[i].hi[d];
+            los[i] = G[i].lo[d];
+            his[i] = G[i].hi[d];
         }
         std::sort(los.begin(), los.end());
         std::sort(his.begin(), his.end());
         for (size_t i = 0; i < n; ++i) {
             // rules whose range meets rule i's on word d: lo <= hi_i, minus those ending below lo_i
-            const size_t a = (size_t)(std::upper_bound(los.begin(), los.end(), R[i].hi[d]) - los.begin());
-            const size_t b = (size_t)(std::lower_bound(his.begin(), his.end(), R[i].lo[d]) - his.begin());
+            const size_t a = (size_t)(std::upper_bound(los.begin(), los.end(), G[i].hi[d]) - los.begin());
+            const size_t b = (size_t)(std::lower_bound(his.begin(), his.end(), G[i].lo[d]) - his.begin());
             const uint32_t ov = (uint32_t)(a - b);
             if (ov < best[i]) {
                 best[i] = ov;
@@ -3605,13 +3620,60 @@ bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t 
     return true;
 }
 
-// The forests of both family lists (l4 / l6: sorted indexes of the list entries), after a
-// directory: node 0 = {trees of family 4, trees of family 6}, node 1 = the families' default
-// answers (list positions, kNone = none), then a copy of each tree's root (family 4's trees
-// first), so that a walk starts without an indirection.
-bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
-                const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, uint32_t binth,
-                size_t node_budget, TreeImage& img) {
+// Binary nodes (build_tree_family: inner {dim | child << 5, threshold}, leaf {16 | count << 5,
+// first entry}) -> the walk's two-level nodes (Args::tree comment), breadth first from the roots
+// (roots[k] -> node first + k).  False when an index outgrows its bits.
+bool pack_two_level(const std::vector<uint2>& bin, const std::vector<uint32_t>& roots,
+                    uint32_t first, std::vector<uint4>& out) {
+    auto is_leaf = [&](uint32_t b) { return (bin[b].x & 16u) != 0u; };
+    auto leaf_word = [&](uint32_t b, bool& ok) {
+        const uint32_t cnt = bin[b].x >> 5, off = bin[b].y;
+        ok = ok && cnt < (1u << 11) && off < (1u << 21);
+        return cnt << 21 | off;
+    };
+    out.resize(first + roots.size(), make_uint4(0, 0, 0, 0));
+    std::deque<std::pair<uint32_t, uint32_t>> q;   // (binary node, packed node)
+    for (size_t k = 0; k < roots.size(); ++k) q.emplace_back(roots[k], first + (uint32_t)k);
+    bool ok = true;
+    while (!q.empty() && ok) {
+        const auto [b, o] = q.front();
+        q.pop_front();
+        if (is_leaf(b)) {
+            out[o] = make_uint4(1u << 12, leaf_word(b, ok), 0, 0);
+            continue;
+        }
+        const uint32_t l = bin[b].x >> 5, r = l + 1;
+        const bool ll = is_leaf(l), rl = is_leaf(r);
+        const uint32_t base = (ll && rl) ? 0u : (uint32_t)out.size();
+        ok = ok && base < (1u << 17);
+        uint4 nd;
+        nd.x = (bin[b].x & 15u) | (bin[l].x & 15u) << 4 | (bin[r].x & 15u) << 8 |
+               (ll ? 1u : 0u) << 13 | (rl ? 1u : 0u) << 14 | base << 15;
+        nd.y = bin[b].y;
+        nd.z = ll ? leaf_word(l, ok) : bin[l].y;
+        nd.w = rl ? leaf_word(r, ok) : bin[r].y;
+        out[o] = nd;
+        uint32_t next = base;
+        for (const uint32_t c : {l, r}) {
+            if (is_leaf(c)) continue;
+            out.resize(out.size() + 2, make_uint4(0, 0, 0, 0));
+            q.emplace_back(bin[c].x >> 5, next);
+            q.emplace_back((bin[c].x >> 5) + 1u, next + 1u);
+            next += 2;
+        }
+    }
+    return ok;
+}
+
+// The forests of both family lists (l4 / l6: sorted indexes of the list entries), packed two
+// levels to a node after the directory (Args::tree comment: node 0 = {trees of family 4, trees
+// of family 6 | IPv6 byte orders << 16, the families' default answers (list positions, kNone =
+// none)}, then the trees' roots, family 4's first, so that a walk starts without an indirection).
+// group_be: the IPv6 rules grouped by their big-endian ranges whatever the words' byte order
+// (build_tree's choice).
+bool build_tree_as(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                   const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, uint32_t binth,
+                   size_t node_budget, bool group_be, TreeImage& img) {
     img = TreeImage();
     TreeImage body;
     std::vector<TreeRule> R;
@@ -3622,16 +3684,18 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     R.clear();
     const uint32_t swap6 = tree_swap6(v4, v6, l6);
     for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i], swap6));
-    if (!build_forest_family(R, 1, binth, node_budget, body, r6, &def6)) return false;
-    const uint32_t dir = 2u + (uint32_t)(r4.size() + r6.size());
-    auto shift = [&](uint2 nd) {   // inner nodes' child indexes move by the directory's size
-        return (nd.x & 16u) ? nd : make_uint2((nd.x & 15u) | (((nd.x >> 5) + dir) << 5), nd.y);
-    };
-    img.nodes.push_back(make_uint2((uint32_t)r4.size(), (uint32_t)r6.size() | swap6 << 16));
-    img.nodes.push_back(make_uint2(def4, def6));
-    for (uint32_t r : r4) img.nodes.push_back(shift(body.nodes[r]));
-    for (uint32_t r : r6) img.nodes.push_back(shift(body.nodes[r]));
-    for (uint2 nd : body.nodes) img.nodes.push_back(shift(nd));
+    std::vector<TreeRule> RG;
+    if (group_be)
+        for (uint32_t i : l6) RG.push_back(tree_rule(6, v4[i], &v6[i], 0xFFu));
+    if (!build_forest_family(R, 1, binth, node_budget, body, r6, &def6, group_be ? &RG : nullptr))
+        return false;
+    std::vector<uint32_t> roots = r4;
+    roots.insert(roots.end(), r6.begin(), r6.end());
+    std::vector<uint4> packed;
+    if (!pack_two_level(body.nodes, roots, 1u, packed)) return false;
+    packed[0] = make_uint4((uint32_t)r4.size(), (uint32_t)r6.size() | swap6 << 16, def4, def6);
+    img.nodes.resize(2 * packed.size());
+    memcpy(img.nodes.data(), packed.data(), packed.size() * sizeof(uint4));
     img.leaves = std::move(body.leaves);
     img.depth[0] = body.depth[0];
     img.depth[1] = body.depth[1];
@@ -3639,7 +3703,79 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
     img.trees[0] = (uint32_t)r4.size();
     img.trees[1] = (uint32_t)r6.size();
     img.swap6 = swap6;
-    return img.nodes.size() < (1u << 27);
+    return true;
+}
+
+uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
+                        const std::vector<RuleV6>& v6, const std::vector<uint32_t>& list, bool is6,
+                        const uint32_t kv[kTreeDims], uint32_t k0, uint32_t k1, const uint32_t s[4],
+                        const uint32_t d[4], uint8_t* prof_depth, uint8_t* prof_steps);
+
+// Sampled walk cost of an image's IPv6 forest: nodes loaded plus leaf entries read (tree_walk_host's
+// profile) over keys whose fields are drawn from the IPv6 rules' own constrained fields, a stand-in
+// for traffic from the pools the rules were written for.
+uint64_t tree_sample_cost6(const TreeImage& img, const std::vector<RuleV4>& v4,
+                           const std::vector<RuleV6>& v6, const std::vector<uint32_t>& l6) {
+    static constexpr int kFieldDims[5][2] = {{0, 4}, {4, 8}, {8, 9}, {9, 10}, {10, 11}};
+    std::vector<TreeRule> R;
+    for (uint32_t i : l6) R.push_back(tree_rule(6, v4[i], &v6[i], img.swap6));
+    std::vector<uint32_t> by_field[5];
+    for (uint32_t i = 0; i < (uint32_t)R.size(); ++i)
+        for (int f = 0; f < 5; ++f)
+            for (int dm = kFieldDims[f][0]; dm < kFieldDims[f][1]; ++dm)
+                if (R[i].lo[dm] != 0 || R[i].hi[dm] != kTreeWidth[dm]) {
+                    by_field[f].push_back(i);
+                    break;
+                }
+    uint64_t x = 0x9E3779B97F4A7C15ull, cost = 0;
+    auto rnd = [&]() {   // splitmix64
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return (uint32_t)(z ^ (z >> 31));
+    };
+    const size_t n = std::min<size_t>(4096, 4 * R.size());
+    for (size_t k = 0; k < n; ++k) {
+        uint32_t kv[kTreeDims] = {};
+        for (int f = 0; f < 5; ++f) {
+            const TreeRule* r = by_field[f].empty() ? nullptr : &R[by_field[f][rnd() % by_field[f].size()]];
+            for (int dm = kFieldDims[f][0]; dm < kFieldDims[f][1]; ++dm) {
+                const uint32_t lo = r ? r->lo[dm] : 0u, hi = r ? r->hi[dm] : kTreeWidth[dm];
+                const uint64_t span = (uint64_t)hi - lo + 1u;
+                kv[dm] = lo + (uint32_t)(rnd() % span);
+            }
+        }
+        uint32_t sw[4], dw[4];
+        for (int j = 0; j < 4; ++j) {
+            sw[j] = word_of(kv[j], img.swap6, j);
+            dw[j] = word_of(kv[4 + j], img.swap6, 4 + j);
+        }
+        const uint32_t k0 = 6u | kv[10] << 8 | kv[8] << 16, k1 = kv[9];
+        uint8_t dep[16] = {}, stp[16] = {};
+        tree_walk_host(img, v4, v6, l6, true, kv, k0, k1, sw, dw, dep, stp);
+        for (int t = 0; t < 16; ++t) cost += dep[t] + stp[t];
+    }
+    return cost;
+}
+
+// build_tree_as, and when the IPv6 words' byte orders differ from big-endian, also with the
+// grouping by big-endian ranges: the one of lower sampled cost (tree_sample_cost6).  The byte
+// order makes a version-agnostic IPv4 prefix a range (config C6: 75 -> 63 us per 1M), but the
+// grouping its ranges imply can move rules into port and protocol trees with long leaves (the
+// 16k-rule flow table: 269 -> 332 us; the big-endian grouping 260).
+bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, uint32_t binth,
+                size_t node_budget, TreeImage& img) {
+    const bool ok = build_tree_as(v4, v6, l4, l6, binth, node_budget, false, img);
+    if (!ok || img.swap6 == 0xFFu) return ok;
+    TreeImage alt;
+    if (!build_tree_as(v4, v6, l4, l6, binth, node_budget, true, alt)) return true;
+    const uint64_t ca = tree_sample_cost6(img, v4, v6, l6), cb = tree_sample_cost6(alt, v4, v6, l6);
+    if (getenv("UPE_GPU_VERBOSE"))
+        fprintf(stderr, "upe_gpu: tree IPv6 byte orders %02x, sampled cost %llu (grouped as such) / %llu (grouped big-endian)\n",
+                img.swap6, (unsigned long long)ca, (unsigned long long)cb);
+    if (cb < ca) img = std::move(alt);
+    return true;
 }
 
 // The tree of a table: the shortest leaves (at most 1, 2, 3, then kTreeBinth rules before a
@@ -3670,25 +3806,38 @@ bool choose_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
 uint32_t tree_walk_host(const TreeImage& img, const std::vector<RuleV4>& v4,
                         const std::vector<RuleV6>& v6, const std::vector<uint32_t>& list, bool is6,
                         const uint32_t kv[kTreeDims], uint32_t k0, uint32_t k1, const uint32_t s[4],
-                        const uint32_t d[4], uint8_t* prof_depth = nullptr,
-                        uint8_t* prof_steps = nullptr) {
+                        const uint32_t d[4], uint8_t* prof_depth, uint8_t* prof_steps) {
     const uint2 dir = img.nodes[0], dflt = img.nodes[1];
-    const uint32_t nt = is6 ? dir.y & 0xFFFFu : dir.x, first = 2u + (is6 ? dir.x : 0u);
+    const uint32_t nt = is6 ? dir.y & 0xFFFFu : dir.x, first = 1u + (is6 ? dir.x : 0u);
+    const uint4* S = reinterpret_cast<const uint4*>(img.nodes.data());
     uint32_t best = kNone;
     for (uint32_t t = 0; t < nt; ++t) {
-        uint2 nd = img.nodes[first + t];
-        uint32_t depth = 0;
-        while (!(nd.x & 16u)) {
-            nd = img.nodes[(nd.x >> 5) + (kv[nd.x & 15u] >= nd.y ? 1u : 0u)];
+        uint32_t idx = first + t, lw = 0, depth = 0;
+        for (;;) {   // tree_match's step, two levels per node
+            const uint4 q = S[idx];
             ++depth;
+            if (q.x & 0x1000u) {
+                lw = q.y;
+                break;
+            }
+            const bool c1 = kv[q.x & 15u] >= q.y;
+            const bool lleaf = (q.x >> 13) & 1u;
+            const bool cl = c1 ? ((q.x >> 14) & 1u) != 0u : lleaf;
+            const uint32_t ct = c1 ? q.w : q.z;
+            if (cl) {
+                lw = ct;
+                break;
+            }
+            const uint32_t c2 = kv[c1 ? (q.x >> 8) & 15u : (q.x >> 4) & 15u] >= ct ? 1u : 0u;
+            idx = (q.x >> 15) + ((c1 && !lleaf) ? 2u : 0u) + c2;
         }
-        const uint32_t cnt = nd.x >> 5;
+        const uint32_t cnt = lw >> 21, off = lw & 0x1FFFFFu;
         if (prof_depth && t < 16) {
             prof_depth[t] = (uint8_t)std::min(depth, 255u);
             prof_steps[t] = 0;
         }
         for (uint32_t j = 0; j < cnt; ++j) {
-            const uint32_t e = img.leaves[nd.y + j];
+            const uint32_t e = img.leaves[off + j];
             const uint32_t pos = e & 0x7FFFFFFFu;
             if (prof_steps && t < 16 && prof_steps[t] < 255) ++prof_steps[t];
             if (pos >= best) break;
