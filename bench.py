@@ -11,10 +11,11 @@ the 64 B and IMIX rates come out of the same run at each GPU count.  Every step 
 batch (the path rewrites TTL / checksum / MACs in place, so re-running a batch would change the
 work), which also keeps the working set past the 256 MiB Infinity Cache: inputs come from HBM.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
-per GPU, each with its own static shard of the packet stream (a full config-B batch per step,
-tables replicated), no data-path collective — weak scaling.  torch.distributed carries only the
-barrier and the max-over-ranks time.
+Multi-GPU (`python bench.py --gpus N`, which starts the N ranks under torch.distributed.run
+itself, or the same launcher run by the caller): one process per GPU, each with its own static
+shard of the packet stream (a full config-B batch per step, tables replicated), no data-path
+collective — weak scaling.  torch.distributed carries only the barrier and the max-over-ranks
+time.  The CPU baseline is timed by rank 0 after the timed regions at every N.
 
 After the timed region (never part of `value`): the other output mode, the IMIX leg, the ring
 leg (16 resident batches per launch), the achievable-bandwidth probe, and the host-inclusive legs
@@ -169,15 +170,56 @@ def rule_index_name(kind: int) -> str:
     return {0: "linear scan", 1: "tuple-space index", 2: "decision tree"}.get(kind, str(kind))
 
 
-def pmc_traffic(config: str, packets: int, mode: str):
-    """HBM bytes per classify launch from the committed PMC passes of this kernel
-    (profiles/pmc_config<X>[_emit].json, made by tools/pmc_run.sh + tools/pmc_traffic.py), or
-    None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_config{config}{'_emit' if mode == 'emit' else ''}.json")
+PMC_DIR = os.path.join("profiles", "r06")   # the committed PMC summaries of this round's build
+
+
+def lib_sha16() -> str | None:
+    """sha256 (first 16 hex digits) of the libupe_gpu.so this process loads."""
+    import hashlib
+
+    try:
+        return hashlib.sha256(open(os.path.join(ROOT, "upe_amd", "libupe_gpu.so"),
+                                   "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_record(label: str, packets: int, mode: str):
+    """The committed PMC summary of this leg's classify kernel (profiles/r06/pmc_<label>_<mode>.json,
+    made by tools/pmc_refresh.sh + tools/pmc_r06.py from separate FETCH_SIZE / WRITE_SIZE / SQ /
+    GRBM passes), or None when there is none for this batch size."""
+    rel = os.path.join(PMC_DIR, f"pmc_{label}_{mode}.json")
+    path = os.path.join(ROOT, rel)
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
-    return d["traffic_bytes_per_launch"] if d.get("packets") == packets else None
+    if d.get("packets") != packets:
+        return None
+    d["source"] = rel
+    return d
+
+
+def pmc_traffic(label: str, packets: int, mode: str):
+    """HBM bytes per classify launch (2 x FETCH_SIZE + WRITE_SIZE) from pmc_record, or None."""
+    d = pmc_record(label, packets, mode)
+    return d.get("traffic_bytes_per_launch") if d else None
+
+
+def traffic_note(label: str, packets: int, mode: str):
+    """Where roofline.traffic came from: the summary file, its passes' UTC stamps, and whether
+    its profiled library is the one this run loaded (same sha256)."""
+    d = pmc_record(label, packets, mode)
+    if not d or "traffic_bytes_per_launch" not in d:
+        return None
+    return {"file": d["source"], "lib_sha16": d.get("lib_sha16"),
+            "same_build_as_this_run": d.get("lib_sha16") == lib_sha16(),
+            "passes_utc": {g: (s.split("utc=")[-1] if s else None)
+                           for g, s in d.get("passes", {}).items()},
+            "read_bytes_per_packet": d.get("read_bytes_per_packet"),
+            "write_bytes_per_packet": d.get("write_bytes_per_packet"),
+            "wave_time": d.get("wave_time"),
+            "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, 2 x "
+                      "FETCH_SIZE + WRITE_SIZE (gfx950), median full-batch dispatch"}
 
 
 def cpu_quota():
@@ -295,9 +337,12 @@ def dropin_pipeline(local: list | None, seconds: float = 2.0, device: int = 0) -
                                       seconds, 65536, cpus, out)
             legs.append({"workers": (f"{workers} GPU worker(s), " +
                                      ("pktbufs classified in the registered pool (mapped)"
-                                      if mapped else "header windows via the DMA round trip"))
+                                      if mapped else "header windows staged in pinned memory, "
+                                      "read there by the kernel"))
                          if gpu else f"{workers} reference worker thread(s) (src/worker.c)",
                          "pool": pool, "ring": ring, "rc": rc,
+                         "gpu_batch": (max(256, min(65536, pool // (4 * workers))) if gpu
+                                       else None),
                          "consumer_mpps": round(out[0], 2), "producer_mpps": round(out[1], 2),
                          "ring_full_events": int(out[2]), "seconds": round(out[3], 3)})
     return {"legs": legs, "packet": "64 B Eth/IPv4/TCP 10.128.0.1:45000 -> 10.128.0.2:80, "
@@ -459,8 +504,8 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "kernel_ms": round(kern_s * 1e3, 5),
                          "algorithmic_bytes_per_packet": round(float(bpp.sum()) / n, 2),
-                         "traffic": pmc_traffic({"C": "CF", "C3": "C", "C6": "C6"}[kind], n,
-                                                mode),
+                         "traffic": pmc_traffic({"C": "CF"}.get(kind, kind), n, mode),
+                         "traffic_source": traffic_note({"C": "CF"}.get(kind, kind), n, mode),
                          "rule_index": rule_index_name(idx_kind)},
             "format": "packed frames (upe_gpu_process_emit)",
             "what": f"all ranks at once after the main region, {copies} distinct batch copies "
@@ -523,15 +568,14 @@ def strong_leg(torch, dev, dist, rank: int, world: int, local: int, kind: str, s
 VALU_PEAK_G = 1024 * 2.4 / 2   # G wave64 VALU instructions/s: 1024 SIMD-32s, one per 2 cycles
 
 
-def pmc_valu(config: str, packets: int, mode: str = "emit"):
-    """The classify kernel's VALU counts per launch from the committed PMC passes
-    (profiles/pmc_config<X>[_emit]_valu.json, tools/pmc_run.sh + tools/pmc_valu.py), or None."""
-    path = os.path.join(ROOT, "profiles",
-                        f"pmc_config{config}{'_emit' if mode == 'emit' else ''}_valu.json")
-    if not os.path.exists(path):
+def pmc_valu(label: str, packets: int, mode: str = "emit"):
+    """The classify kernel's VALU counts per launch from the committed PMC summary
+    (pmc_record: SQ and GRBM passes), or None."""
+    d = pmc_record(label, packets, mode)
+    if not d or "valu_frac" not in d:
         return None
-    d = json.load(open(path))
-    return d if d.get("packets") == packets else None
+    return {"sq_insts_valu": d["sq"]["SQ_INSTS_VALU"], "valu_frac": d["valu_frac"],
+            "valu_insts_per_packet": d["valu_insts_per_64_packets"], "source": d["source"]}
 
 
 def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: int = 8) -> dict:
@@ -596,9 +640,9 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
                      "valu_insts_per_launch": pv["sq_insts_valu"],
                      "frac_pmc_cycles": round(pv["valu_frac"], 4),
                      "valu_wave_insts_per_64_packets": round(pv["valu_insts_per_packet"], 1),
-                     "source": "profiles/pmc_configD_emit_valu.json (rocprofv3 SQ_INSTS_VALU per "
-                               "classify launch) / this run's classify time (HIP events); "
-                               "frac_pmc_cycles: over the PMC run's own GRBM_GUI_ACTIVE cycles"})
+                     "source": pv["source"] + " (rocprofv3 SQ_INSTS_VALU per classify launch) / "
+                               "this run's classify time (HIP events); frac_pmc_cycles: over the "
+                               "PMC run's own GRBM_GUI_ACTIVE cycles"})
     else:
         valu.update({"achieved": None, "frac": None,
                      "source": "no committed VALU PMC summary for this batch size"})
@@ -611,7 +655,7 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
         t_ach = traffic / classify_s / 1e9
         hbm.update({"achieved": round(t_ach, 1), "frac": round(t_ach / HBM_PEAK_GBPS, 4),
                     "source": "bytes requested past L2 per classify launch (PMC, "
-                              "profiles/pmc_configD_emit.json: 2 x FETCH_SIZE + WRITE_SIZE; "
+                              f"{PMC_DIR}/pmc_D_emit.json: 2 x FETCH_SIZE + WRITE_SIZE; "
                               "Infinity-Cache hits included, so an upper bound on HBM bytes) / "
                               "this run's classify time"})
     else:
@@ -623,6 +667,7 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
     # and the counted-bytes rate stay beside it (valu / hbm)
     roof.update({"bound": "hbm", "achieved": hbm["algorithmic"]["achieved"], "peak": HBM_PEAK_GBPS,
                  "unit": "GB/s", "frac": hbm["algorithmic"]["frac"], "traffic": traffic,
+                 "traffic_source": traffic_note("D", n, "emit"),
                  "algorithmic_bytes_per_packet": hbm["algorithmic"]["bytes_per_packet"],
                  "traffic_bytes_per_packet": round(traffic / n, 2) if traffic else None})
     return {"workload": WORKLOADS["D"] + f", {n} packets per step", "value": round(n * steps / elapsed / 1e6, 2),
@@ -690,9 +735,43 @@ def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
                     "not value (value = one launch per batch)"}
 
 
+def launch_cmd(gpus: int, argv: list, port: int) -> list:
+    """The command the parent runs for --gpus N > 1 without a launcher around it: N ranks on
+    this node under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1), each
+    running this file with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(gpus, env) -> int:
+    """The world size this process runs in: WORLD_SIZE when a launcher set it (and then --gpus,
+    if given, must agree), else 1.  Raises SystemExit on a mismatch."""
+    ws = env.get("WORLD_SIZE")
+    world = int(ws) if ws is not None else 1
+    if gpus is not None and ws is not None and gpus != world:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}")
+    return world
+
+
+def launch_ranks(gpus: int, argv: list) -> int:
+    """`python bench.py --gpus N` (N > 1, no WORLD_SIZE): start the N ranks as a child process
+    and return its exit code.  This process never imports torch or touches a GPU; rank 0's JSON
+    line reaches stdout directly (the children inherit it)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return subprocess.run(launch_cmd(gpus, argv, port), cwd=ROOT).returncode
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; N > 1 without a launcher starts N ranks "
+                         "under torch.distributed.run itself (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="B", choices=sorted(WORKLOADS))
@@ -747,10 +826,12 @@ def main() -> None:
     ap.add_argument("--ring", type=int, default=16,
                     help="batches per launch of the ring leg (config B; 0 skips it)")
     args = ap.parse_args()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = world_check(args.gpus, os.environ)
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them round robin
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -766,6 +847,10 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        # a host-side group for the wait while rank 0 times the CPU baseline (no GPU spin)
+        import datetime
+
+        host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
     else:
         torch.cuda.set_device(local)
 
@@ -947,7 +1032,8 @@ def main() -> None:
 
     if rank == 0:
         bpp = algorithmic_bytes(wl, v_first, emit=args.mode == "emit")
-        traffic = pmc_traffic({"C": "CF"}.get(args.config, args.config), n, args.mode)
+        plabel = {"C": "CF"}.get(args.config, args.config)
+        traffic = pmc_traffic(plabel, n, args.mode)
         bytes_per_launch = float(bpp.sum())
         # a step's kernels: the classify launch plus (tables over 4096 rules) the rule_stats
         # group-by; finalize_ms is the group-by's share (0 for smaller tables)
@@ -967,6 +1053,7 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded upe_amd.synth, per-rank shard), resident in HBM",
+            "lib_sha16": lib_sha16(),
             "host_thread": {"cpu": pinned_cpu, "numa_node": numa_node,
                             "gpu_local_cpus": len(local_cpus)},
             "config": {"workload": WORKLOADS[args.config], "packets_per_gpu_step": n,
@@ -983,9 +1070,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "traffic_source": (f"profiles/pmc_config{ {'C': 'CF'}.get(args.config, args.config)}"
-                                   f"{'_emit' if args.mode == 'emit' else ''}.json (rocprofv3 "
-                                   "PMC, 2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
+                "traffic_source": traffic_note(plabel, n, args.mode),
                 "kernel": "upe_classify",
                 "kernel_ms": round(kern_s * 1e3, 5),
                 "classify_ms": round(classify_ms / max(launches, 1), 5),
@@ -1069,15 +1154,22 @@ def main() -> None:
                                     "(upe_gpu_process_mapped" + ("_emit" if h["emit"] else "") +
                                     "); " + what + f"; median of {h['reps']} passes, all ranks "
                                     "at once"}
-        if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
-            # config A is the reference's one-worker pcap replay: time it on one core
+        if not args.no_cpu_baseline:
+            # rank 0, after every timed region; at N > 1 the other ranks wait at a host barrier.
+            # Config A is the reference's one-worker pcap replay: time it on one core
             out["cpu_baseline"] = cpu_baseline(wl, 1 if args.config == "A" else args.cpu_threads,
-                                               local_cpus)
-            if args.config == "B" and args.dropin_seconds > 0:
+                                               local_cpus, numa_all=world == 1)
+            if world > 1:
+                out["cpu_baseline"]["ranks_note"] = (
+                    f"timed by rank 0 on its own host cores after the {world}-rank timed regions, "
+                    "the other ranks idle at a host barrier; the same per-host sample as at N=1")
+            if args.config == "B" and args.dropin_seconds > 0 and world == 1:
                 dp = dropin_pipeline(local_cpus, args.dropin_seconds, local)
                 if dp:
                     out["dropin_pipeline"] = dp
         print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier(group=host_group)
     worker.close()
     if dist:
         dist.destroy_process_group()

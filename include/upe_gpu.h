@@ -404,7 +404,13 @@ typedef struct upe_worker_ops {
     int (*sync)(void *user, upe_gpu_ctx_t *ctx);
     /* optional: after every GPU batch walked, and after every sync(), the loop's counters so far
      * (the worker_t fields the stats thread reads, src/main.c:284-315: pkts_in, pkts_parsed,
-     * pkts_matched, pkts_forwarded, pkts_dropped; the rest as upe_counters_t defines them) */
+     * pkts_matched, pkts_forwarded, pkts_dropped; the rest as upe_counters_t defines them).
+     * ctx is NULL while a later batch is still on the GPU: the context's statistics then already
+     * hold some packets the counters do not, so publish the counters only (and never call into
+     * the context, which would wait for that batch).  ctx is the context when nothing is in
+     * flight — after a drain (empty ring, a table-writing packet, a polled change) and at least
+     * every 32 batches of a stream that never drains — and upe_gpu_get_stats(ctx, ...) then
+     * matches the counters packet for packet (rule_stats packets sum to pkts_matched). */
     void (*publish)(void *user, upe_gpu_ctx_t *ctx, const upe_counters_t *counters);
     /* optional: the handles of a burst's forwarded frames after its tx_send_batch, in one call
      * (else free_buf on each; src/worker.c:300-302 frees them one by one) */
@@ -414,9 +420,10 @@ typedef struct upe_worker_ops {
 typedef struct {
     size_t batch;       /* most packets per GPU batch (0 = 65536) */
     unsigned burst;     /* most handles per pop (0 = 32, WORKER_BURST_SIZE; at most 64) */
-    /* NULL: each packet's first UPE_HDR_WINDOW bytes are copied into pinned staging, shipped
-     * with the descriptors, classified in emit mode, and the verdicts and records come back
-     * (records applied to the buffers in the walk).  Non-NULL: every buffer's frame lies at
+    /* NULL: each packet's first UPE_HDR_WINDOW bytes are copied into pinned staging and
+     * classified there by upe_gpu_process_mapped_emit (the kernel reads the windows over the
+     * link; no DMA copies), the verdicts and records written to pinned host memory (records
+     * applied to the buffers in the walk).  Non-NULL: every buffer's frame lies at
      * pool_base + a multiple of 16, inside memory registered with upe_gpu_host_register (e.g.
      * the reference's pktbuf pool), and each batch is classified where it lies by
      * upe_gpu_process_mapped_emit (nothing copied; the records, written to pinned host memory,

@@ -137,9 +137,11 @@ static void op_publish(void *u, upe_gpu_ctx_t *ctx, const upe_counters_t *c) {
     /* rule_stats into the array the stats thread reads — unless a swap has begun: the packets
      * just classified ran with the old table, and w->rule_stats may already be the new array
      * (swapped before rt, src/main.c:261-263), so both pointers must still be the loaded ones */
+    /* (ctx NULL: a batch is still on the GPU and the context's statistics run ahead of these
+     * counters — counters only; the loop publishes with the context at least every 32 batches) */
     const uint64_t t = now_ns();
     rule_stat_t *rs = __atomic_load_n(&w->rule_stats, __ATOMIC_ACQUIRE);
-    if (rs == g->stats_loaded && __atomic_load_n(&w->rt, __ATOMIC_ACQUIRE) == g->rt_loaded &&
+    if (ctx && rs == g->stats_loaded && __atomic_load_n(&w->rt, __ATOMIC_ACQUIRE) == g->rt_loaded &&
         t - g->stats_last_ns >= g->stats_every_ns) {
         g->stats_last_ns = t;
         (void)upe_gpu_get_stats(ctx, NULL, (upe_rule_stat_t *)rs, g->rt_loaded->capacity);
@@ -344,8 +346,8 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     g.cfg.pool_base = g_mapped ? (uint8_t *)pool.buffers : NULL;
     g.cfg.pool_bytes = g_mapped ? pool.capacity * sizeof(pktbuf_t) : 0;
     g.cfg.batch = 65536;
-    /* (rule_stats published after every batch, so that the array swapped out at a reload holds
-     * exactly the counts up to the swap) */
+    /* (rule_stats published whenever nothing is in flight: at the drain the ring empties into
+     * before the reload below, so the array swapped out holds exactly the counts up to the swap) */
     static upe_worker_ops_t ops;
     ops = g_ops;
     ops.pop_burst = op_pop_logged;
@@ -514,7 +516,13 @@ int upe_dropin_bench(int gpu, int mapped, int workers, int device, size_t pool_c
             gs[i].device = device;
             gs[i].cfg.pool_base = mapped ? (uint8_t *)pool.buffers : NULL;
             gs[i].cfg.pool_bytes = mapped ? pool.capacity * sizeof(pktbuf_t) : 0;
-            gs[i].cfg.batch = gpu_batch;
+            /* a batch the pool can fill: two batches in flight per GPU worker plus the ring's
+             * share stay under the pool (else every batch ends at an empty ring) */
+            {
+                size_t cap = pool.capacity / (4u * (unsigned)workers);
+                if (cap < 256) cap = 256;
+                gs[i].cfg.batch = gpu_batch < cap ? gpu_batch : cap;
+            }
             gs[i].stats_every_ns = 100000000ull; /* rule_stats for the stats thread: 10 Hz */
             if (gpu_worker_start(&gs[i], &th[i]) != 0) return -1;
         } else if (worker_start(&ws[i]) != 0) {

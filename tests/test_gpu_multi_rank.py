@@ -98,15 +98,18 @@ def test_two_rank_static_shards_on_gpu(case, emit):
 
 
 def test_bench_two_ranks():
-    """bench.py's N > 1 path end to end: torch.distributed.run with two ranks on the one GPU
-    (gloo for the barrier and the max / sum over ranks, as UPE_BENCH_DIST_BACKEND allows on a
-    one-GPU box), config B plus the IMIX leg, each rank its own shard (weak scaling), and the
-    strong-scaling leg: one B and one C batch split into the two ranks' contiguous shards."""
+    """bench.py's N > 1 path end to end, started the way the driver starts N = 1: plain
+    `python bench.py --gpus 2`, which launches its two ranks itself (here on the one GPU, gloo
+    for the barrier and the max / sum over ranks, as UPE_BENCH_DIST_BACKEND allows on a one-GPU
+    box): config B plus the IMIX leg, each rank its own shard (weak scaling), the strong-scaling
+    leg (one B and one C batch split into the two ranks' contiguous shards) and rank 0's CPU
+    baseline after the timed regions."""
     env = dict(os.environ, UPE_BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
-           "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-hbm-probe",
-           "--max-copies", "24", "--imix-copies", "8", "--imix-v6fwd", "0"]
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2",
+           "--steps", "20", "--warmup", "5", "--no-hbm-probe", "--cpu-threads", "2",
+           "--dropin-seconds", "0", "--max-copies", "24", "--imix-copies", "8",
+           "--imix-v6fwd", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -119,4 +122,7 @@ def test_bench_two_ranks():
         st = d["strong"][k]
         assert st["scaling"] == "strong" and st["value"] > 0
         assert st["packets_per_step"] == 1 << 20 and st["packets_this_rank"] == 1 << 19
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and "ranks_note" in cb
     print(json.dumps({k: d[k] for k in ("value", "ms_per_step", "n_gpus")}))
+

@@ -31,7 +31,7 @@ def _expected_hashes(wl):
 
 
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
-                                  "config_d_small", "edge_zero", "ndp_walk"])
+                                  "config_cf_small", "config_d_small", "edge_zero", "ndp_walk"])
 def test_flow_hash_in_pass(gpu_worker_factory, case):
     wl, ref = golden_io.load(case)
     w = gpu_worker_factory(wl.capacity)
@@ -89,7 +89,7 @@ def test_egress_list_in_order(gpu_worker_factory, n, code):
 
 @pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
-                                  "config_d_small"])
+                                  "config_cf_small", "config_d_small"])
 def test_egress_list_matches_reference_order(gpu_worker_factory, case, emit):
     """The FWD list (and the DROP_RULE list) built on the device from the GPU's verdicts equals
     the order in which the REFERENCE worker queued those packets: the indexes whose golden

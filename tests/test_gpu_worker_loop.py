@@ -4,8 +4,8 @@ no reference build involved.  Against the restated worker (oracle/cpu_ref.c, in-
 writes): the counters worker_main keeps, rule_stats, every packet's bytes, the neighbour tables
 after the learning packets, and the calls worker_main makes per popped burst (tx_send of answered
 ARP requests, one tx_send_batch of the burst's forwarded frames in packet order,
-src/worker.c:40-52, 240-243, 287-303); in both batch paths (header windows through the DMA round
-trip; frames classified where they lie in registered memory) and with bursts cut across GPU
+src/worker.c:40-52, 240-243, 287-303); in both batch paths (header windows staged in pinned memory,
+read there by the kernel; frames classified where they lie in registered memory) and with bursts cut across GPU
 batches.  Also the loop's argument checks."""
 from __future__ import annotations
 
@@ -44,6 +44,10 @@ class Pipeline:
         self.arp, self.ndp = wl.arp.copy(), wl.ndp.copy()
         self.mapped = mapped
         self.published = 0
+        # publishes with the context (nothing in flight): (pkts_matched, rule_stats packets)
+        self.points = []
+        self.in_flight_publishes = 0
+        self.stats_cap = wl.capacity
         # reload = (sorted table B, capacity B, at): the program swaps the table between the
         # burst that ends before packet `at` and the one that starts there
         self.reload = reload
@@ -115,7 +119,17 @@ class Pipeline:
                                               self.ndp.ctypes.data, len(self.ndp))
 
         def publish(user, ctx, counters):
+            from upe_amd.layout import RULE_STAT_DTYPE
+
             self.published += 1
+            c = np.frombuffer(ctypes.string_at(counters, gpu.COUNTERS_DTYPE.itemsize),
+                              gpu.COUNTERS_DTYPE)
+            if not ctx:
+                self.in_flight_publishes += 1
+                return
+            st = np.zeros(self.stats_cap, RULE_STAT_DTYPE)
+            if gpu.LIB.upe_gpu_get_stats(ctx, None, st.ctypes.data, self.stats_cap) == 0:
+                self.points.append((int(c["pkts_matched"][0]), int(st["packets"].sum())))
 
         self.ops = gpu.WorkerOps(
             gpu.POP_FN(pop), gpu.STOP_FN(lambda u: 1), gpu.DATA_FN(data), gpu.LEN_FN(length),
@@ -227,6 +241,53 @@ def test_worker_loop_rule_reload(gpu_worker_factory, name, mapped):
     assert got == want
     assert np.array_equal(st, rb.rule_stats)
     assert np.array_equal(p.frames(), rb.frames)
+    p.pool.free()
+
+
+@pytest.mark.parametrize("mapped", [False, True], ids=["windows", "mapped"])
+def test_worker_loop_publish_points(gpu_worker_factory, mapped):
+    """with two batches in flight the loop publishes the counters alone (NULL
+    context) and never calls into the context then; at points with nothing in flight (at least
+    every 32 batches of a stream that never drains, and at the final drain) it passes the context,
+    and the rule_stats read there sum exactly to the published pkts_matched."""
+    wl = synth.config_b(n=20_000, seed=84)
+    p = Pipeline(wl, [32], mapped)
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        counters = p.run(w, 64)          # 313 batches of 64 packets, the ring never empty
+    finally:
+        w.close()
+    batches = -(-wl.n // 64)
+    assert p.in_flight_publishes >= batches // 2
+    assert len(p.points) >= batches // 32
+    assert all(m == s for m, s in p.points), p.points[:8]
+    assert p.points[-1][0] == int(counters["pkts_matched"][0])
+    assert sorted(p.freed) == list(range(wl.n))
+    p.pool.free()
+
+
+def test_worker_loop_failure_with_batches_in_flight(gpu_worker_factory):
+    """a frame the loop must refuse (not 16-byte aligned inside the registered pool)
+    several batches into a mapped stream of 4-packet batches, with two batches in flight: the call
+    fails, and every popped handle is freed exactly once (the in-flight batches after the GPU is
+    done with them, the rest of the burst, the TX queue)."""
+    wl = synth.config_b(n=2_000, seed=85)
+    p = Pipeline(wl, [7, 32, 5], True)
+    bad = 301
+    p.off[bad] += 8                   # its frame moves 8 bytes: no longer 16-byte aligned
+    p.pool.array[p.off[bad]:p.off[bad] + p.lens[bad]] = \
+        wl.frames[desc_offsets(wl.desc)[bad]:desc_offsets(wl.desc)[bad] + p.lens[bad]]
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        with pytest.raises(gpu.UpeGpuError, match="16-byte aligned"):
+            p.run(w, 4)
+    finally:
+        w.close()
+    popped = sum(p.pops)
+    assert popped > bad
+    assert sorted(p.freed) == list(range(popped)), "a popped handle freed twice or never"
     p.pool.free()
 
 

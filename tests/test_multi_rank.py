@@ -94,3 +94,31 @@ def test_shard_workload_frames_rebased():
             o, ln = int(desc_offsets(sh.desc)[i]), int(desc_lens(sh.desc)[i])
             go = int(desc_offsets(wl.desc)[s + i])
             assert np.array_equal(sh.frames[o:o + ln], wl.frames[go:go + ln])
+
+
+def test_bench_launcher_command():
+    """`python bench.py --gpus N` (no WORLD_SIZE) starts N ranks under torch.distributed.run on
+    127.0.0.1 with the same arguments; a rank refuses a --gpus that disagrees with WORLD_SIZE.
+    Neither needs torch or a GPU in the launching process."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "20"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29500" in cmd and cmd[-4:] == ["--gpus", "8", "--steps", "20"]
+    assert cmd[-5].endswith("bench.py")
+    assert bench.world_check(None, {}) == 1
+    assert bench.world_check(1, {}) == 1
+    assert bench.world_check(None, {"WORLD_SIZE": "4"}) == 4
+    assert bench.world_check(4, {"WORLD_SIZE": "4"}) == 4
+    with pytest.raises(SystemExit):
+        bench.world_check(4, {"WORLD_SIZE": "2"})
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "1"], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr

@@ -245,7 +245,8 @@ def test_restated_vs_reference_fresh_seeds(seed):
         assert a.l1.tobytes() == b.l1.tobytes()
 
 
-@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "edge_zero", "ndp_walk"])
+@pytest.mark.parametrize("case", ["config_b_small", "config_c_small", "config_cf_small",
+                                  "edge_zero", "ndp_walk"])
 def test_restated_flow_hash_matches_reference(case):
     """The restated parse + flow_hash (oracle/cpu_ref.c) equals the reference's own
     parse_flow_key + flow_hash per packet (tests/golden/flow_hash.npz, from oracle/_ref) — the

@@ -7,7 +7,13 @@ into legs at gaps longer than --gap-ms (the IMIX leg starts after its batch is g
 host, seconds later) and prints count / mean / min / max per leg, so that each leg's mean can
 be set beside the bench line's kernel_ms.
 
-Usage: python tools/kernel_legs.py <p_kernel_trace.csv | run_results.db> [--gap-ms 50] [--match upe_]
+Full-batch means: a leg also holds the small launches of the same instantiation (the first
+warm-up batch, census probes, the host legs' chunks), which drag rocprof's plain mean down.
+Dispatches shorter than --min-frac x the leg's median are dropped from the `full_*` columns
+(and counted in `small`), so that full_mean_us is the mean over full-size batches only.
+
+Usage: python tools/kernel_legs.py <p_kernel_trace.csv | run_results.db> [--gap-ms 50]
+       [--match upe_] [--min-frac 0.5]
 """
 from __future__ import annotations
 
@@ -46,13 +52,18 @@ def main() -> None:
     ap.add_argument("trace")
     ap.add_argument("--gap-ms", type=float, default=50.0)
     ap.add_argument("--match", default="upe_")
+    ap.add_argument("--min-frac", type=float, default=0.5)
     a = ap.parse_args()
-    print(f"{'kernel':100s} {'leg':>3s} {'calls':>6s} {'mean_us':>9s} {'min_us':>9s} {'max_us':>9s}")
+    print(f"{'kernel':100s} {'leg':>3s} {'calls':>6s} {'mean_us':>9s} {'min_us':>9s} "
+          f"{'max_us':>9s} {'small':>6s} {'full_n':>6s} {'full_mean_us':>12s} {'full_min_us':>11s}")
     for name, segs in legs(a.trace, a.gap_ms, a.match).items():
         for i, seg in enumerate(segs):
             d = [(e - s) / 1e3 for s, e in seg]
+            cut = a.min_frac * statistics.median(d)
+            full = [x for x in d if x >= cut]
             print(f"{name[:100]:100s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
-                  f"{min(d):9.2f} {max(d):9.2f}")
+                  f"{min(d):9.2f} {max(d):9.2f} {len(d) - len(full):6d} {len(full):6d} "
+                  f"{statistics.mean(full):12.2f} {min(full):11.2f}")
 
 
 if __name__ == "__main__":

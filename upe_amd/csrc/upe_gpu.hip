@@ -108,6 +108,9 @@ constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 // the in-place one, bit 2 also the tuple-space ones (config B emit 26.2 -> 25.4 us per 1M batch;
 // C unchanged; in place +0.3 % with a VGPR spilled, so off; tuple space: D unchanged, with twice
 // the SGPR spills, so off; issued right after the parse instead: B no gain, C 39.0 -> 40.5).
+#ifndef UPE_TREE_MERGE
+#define UPE_TREE_MERGE 1   // tree_match: the five leaves' entries merged in list order (round 6)
+#endif
 #ifndef UPE_MID_PREFETCH
 #define UPE_MID_PREFETCH 1
 #endif
@@ -314,6 +317,7 @@ constexpr uint32_t kTssRatioX2 = 5;   // tuple-space slots >= ratio / 2 x keys
 // IPv6 default answer}), each tree's root node (IPv4 first), the other nodes, then the leaf
 // entries; staged in LDS when it fits beside the launch's other LDS data.
 constexpr int kTreeDims = 11;
+constexpr int kTreeFields = 5;   // field trees per family (build_forest_family)
 constexpr uint32_t kTreeBinth = 4;   // a node with more rules than this is split (if it can be)
 constexpr size_t kTreeMinReach = 64;   // (load_rules_impl: tree or scan)
 
@@ -836,6 +840,7 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
     const bool fam_lds = (a.fam4_lds || a.fam4 == 0u) && (a.fam6_lds || a.fam6 == 0u);
+#if !UPE_TREE_MERGE
     // The leaf of one tree: its rules in list order until a match or a position >= best.
     auto leaf_tests = [&](const uint32_t lw) {
         const uint32_t cnt = lw >> 21, off = lw & 0x1FFFFFu;
@@ -906,6 +911,85 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             }
         }
     };
+#endif
+    // One leaf entry's rule against the key (the flagged covering entry matches without a test):
+    // its FamTable words from LDS (both lists staged: one address, the IPv6 words issued with the
+    // first two) or memory.
+    auto entry_matches = [&](const uint32_t p, const bool cov) -> bool {
+        if (fam_lds) {
+            const uint4* f = is6 ? l6 + kFamV6Stride * p : l4 + 2 * p;
+            const uint4 e0 = f[0], e1 = f[1];
+            uint32_t x6 = 0;
+            if (is6) {
+                const uint4 e2 = f[2], e3 = f[3], e4 = f[4];
+                x6 = ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+                     ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+            }
+            const uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                               ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w) | x6;
+            if (cov || x == 0u) bact = e0.z;
+            return cov || x == 0u;
+        }
+        uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
+        if (is6) {
+            const uint4* f = a.fam6_lds ? l6 + kFamV6Stride * p : g6 + (size_t)kFamV6Stride * p;
+            e0 = f[0];
+            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
+        } else {
+            const uint4* f = a.fam4_lds ? l4 + 2 * p : a.fam + 2 * (size_t)p;
+            e0 = f[0];
+            if (!cov) e1 = f[1];
+        }
+        uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
+                     ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
+        x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
+             ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
+        if (cov || x == 0u) bact = e0.z;
+        return cov || x == 0u;
+    };
+    // The five leaves merged (round 6): each leaf lists its rules in ascending list position and
+    // the trees' rules are disjoint, so taking the smallest next position over the five leaves
+    // visits a lane's candidates in list order, and the first that matches is the answer: no
+    // later entry of any leaf is read.  One loop for the wave (as long as its longest lane's
+    // merged prefix, not the sum over trees of each tree's longest leaf), and one dependent LDS
+    // round trip per step: the chosen leaf's next entry is read together with the rule words.
+    // A head is (position << 1 | covering flag), ~0 when the leaf is exhausted.
+    auto merged_tests = [&](const uint32_t (&lw)[kTreeFields]) {
+        // per leaf: its head, and (entries left after the head) << 21 | the next entry's index
+        uint32_t h[kTreeFields], c[kTreeFields];
+#pragma unroll
+        for (int t = 0; t < kTreeFields; ++t) {
+            const bool any = (lw[t] >> 21) != 0u;
+            h[t] = any ? __builtin_rotateleft32(E[lw[t] & 0x1FFFFFu], 1) : ~0u;
+            c[t] = any ? lw[t] + 1u - (1u << 21) : 0u;
+        }
+        bool look = active;
+        while (__any(look)) {
+            uint32_t m = h[0];
+#pragma unroll
+            for (int t = 1; t < kTreeFields; ++t) m = min(m, h[t]);
+            look = look && m != ~0u;
+            if (look) {
+                // the chosen leaf moves on: its next entry is loaded with the rule words
+                uint32_t cc = 0u;
+#pragma unroll
+                for (int t = 0; t < kTreeFields; ++t) cc = h[t] == m ? c[t] : cc;
+                const uint32_t nxe = (cc >> 21) != 0u
+                                         ? __builtin_rotateleft32(E[cc & 0x1FFFFFu], 1) : ~0u;
+                const uint32_t p = m >> 1;
+                if (entry_matches(p, (m & 1u) != 0u)) {
+                    best = p;
+                    look = false;
+                }
+#pragma unroll
+                for (int t = 0; t < kTreeFields; ++t) {
+                    const bool sel = h[t] == m;
+                    h[t] = sel ? nxe : h[t];
+                    c[t] = sel ? cc + 1u - (1u << 21) : c[t];
+                }
+            }
+        }
+    };
     // an address tree's key word for a dimension: one of its field's words (big-endian for IPv6
     // where the image says so, so that a prefix is a range; IPv4's host-order word 0 and zeros),
     // or a port or the protocol (dimensions 8-10); bit selects keep them in registers
@@ -953,10 +1037,23 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             step(qb, ib, lb, vb, [&](uint32_t dm) { return addr_word(dm, wd); });
             step(qc, ic, lc, vc, [&](uint32_t) { return dp; });
         }
+#if UPE_TREE_MERGE
+        uint32_t ja = first + 2u, jb = first + 4u, ma = 0, mb = 0;
+        bool wa = nt != 0u, wb = wa;
+        while (__any(wa || wb)) {
+            const uint4 qa = S[ja], qb = S[jb];
+            step(qa, ja, ma, wa, [&](uint32_t) { return sp; });
+            step(qb, jb, mb, wb, [&](uint32_t) { return pr; });
+        }
+        const uint32_t lw[kTreeFields] = {la, lb, lc, ma, mb};
+        merged_tests(lw);
+#else
         leaf_tests(la);
         leaf_tests(lb);
         leaf_tests(lc);
+#endif
     }
+#if !UPE_TREE_MERGE
     {
         uint32_t ia = first + 2u, ib = first + 4u, la = 0, lb = 0;
         bool va = nt != 0u, vb = va;
@@ -968,6 +1065,7 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
         leaf_tests(la);
         leaf_tests(lb);
     }
+#endif
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
         const uint2 dflt = N[1];
@@ -3555,7 +3653,6 @@ bool build_tree_family(const std::vector<TreeRule>& R, const std::vector<uint32_
 // is the smallest of its first matches in the trees (the groups partition the list).  The
 // family's first rule that matches every key is no tree's, nor is any rule after it: it is the
 // answer when no tree has one (*def, its list position, else kNone).  roots: kTreeFields entries.
-constexpr int kTreeFields = 5;
 int tree_field(int d) { return d < 4 ? 0 : d < 8 ? 1 : d - 6; }
 constexpr uint32_t kTreeFieldDims[kTreeFields] = {0x70Fu, 0x7F0u, 1u << 8, 1u << 9, 1u << 10};
 bool build_forest_family(const std::vector<TreeRule>& R, int fam_slot, uint32_t binth,
@@ -3785,6 +3882,19 @@ bool build_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
 // at 4 / 3 / 2, whose image no longer fit; C6 83.7 / 79.2 / 76.6).  Tables whose lists cannot be
 // staged anyway get kTreeBinth.  forced: UPE_GPU_TREE_BINTH (diagnostic), 0 = choose.
 constexpr size_t kTreeLdsReserve = 56 * 1024;
+// The list entries a scan of family F's list can reach: up to and including its first rule that
+// matches every key of the family (build_forest_family's default answer), else the whole list.
+size_t scan_reach(int F, const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
+                  const std::vector<uint32_t>& list) {
+    for (size_t j = 0; j < list.size(); ++j) {
+        const TreeRule r = tree_rule(F, v4[list[j]], F == 6 ? &v6[list[j]] : nullptr);
+        bool all = true;
+        for (int d = 0; d < kTreeDims && all; ++d)
+            all = (r.exact >> d & 1u) && r.lo[d] == 0 && r.hi[d] == kTreeWidth[d];
+        if (all) return j + 1;
+    }
+    return list.size();
+}
 size_t tree_node_budget(size_t count);
 bool choose_tree(const std::vector<RuleV4>& v4, const std::vector<RuleV6>& v6,
                  const std::vector<uint32_t>& l4, const std::vector<uint32_t>& l6, size_t count,
@@ -4083,7 +4193,11 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
     std::vector<uint4> timg;
     TreeImage t;
     const char* tf = getenv("UPE_GPU_TREE");
-    if (!tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0')) {
+    // (the reach first, from the lists alone: a table a scan never walks far into is not built a
+    // tree only to throw it away — ADVICE r05; a reload then costs the lists, not the forest)
+    const size_t reach0 = std::max(scan_reach(4, v4, v6, l4), scan_reach(6, v4, v6, l6));
+    if (!tss && pad > (size_t)kSmallRules && !(tf && tf[0] == '0') &&
+        (reach0 > kTreeMinReach || (tf && tf[0] == '1'))) {
         const char* bt = getenv("UPE_GPU_TREE_BINTH");
         const uint32_t binth = bt ? (uint32_t)std::max(1, atoi(bt)) : 0u;
         if (choose_tree(v4, v6, l4, l6, count, binth, t)) {

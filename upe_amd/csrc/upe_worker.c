@@ -24,17 +24,21 @@
  * loop walks batch k - 1's verdicts (the TX calls, the frees) and then gathers batch k + 1 into
  * the slot k - 1 used — the GPU's share of a batch hides behind the host's.  A batch cut at a
  * table-writing packet drains the pipeline instead (walk k - 1, wait for k, walk it, apply the
- * write, upload the tables) before anything later is launched, and so does an empty ring and a
- * change polled between bursts: the order of every call is the sequential loop's.  The walk
+ * write, upload the tables) before anything later is launched, and so does a change polled
+ * between bursts: the order of every call is the sequential loop's.  An empty ring launches the
+ * partial batch gathered so far like a full one (round 6: with the reference's 8192-buffer pool
+ * a 65536-packet batch never fills, and draining at every empty ring serialised the GPU and the
+ * host), and drains only when the ring is still empty on the next pop.  The walk
  * reads nothing of a frame it does not rewrite: the handle's data pointer and length are kept
  * from the gather.
  *
  * Two ways to get a batch to the GPU (cfg->pool_base): copy each frame's header window into
- * pinned staging, ship it with the descriptors, classify in emit mode and bring back the verdicts
- * and 16-byte records (applied to the caller's buffers in the walk, upe_hdr_apply) — or leave the
- * frames where they are in a registered pool, let the kernel read them there over the link and
- * write the verdicts and records into pinned host memory (upe_gpu_process_mapped_emit, nothing
- * copied), the records applied in the walk.  (Rewriting the frames in the pool from the GPU
+ * pinned staging and let the kernel read the windows there over the link (round 6: until round 5
+ * the windows and descriptors went over by DMA and the verdicts and records came back the same
+ * way, four copies per batch whose fixed cost bound the loop at the reference's small pool), or
+ * leave the frames where they are in a registered pool and let the kernel read them there.
+ * Either way the verdicts and 16-byte records are written into pinned host memory
+ * (upe_gpu_process_mapped_emit, nothing copied) and the records applied in the walk.  (Rewriting the frames in the pool from the GPU
  * instead, upe_gpu_process_mapped, measured 50 vs 66 Mpps for one worker thread on the reference
  * benchmark: the link writes evict the frame lines the walk and pktbuf_free then touch.)
  */
@@ -55,6 +59,9 @@ int upe_gpu_tag_host(upe_gpu_ctx_t *ctx, int on);
 
 #define WIN UPE_HDR_WINDOW
 #define NSLOT 2
+/* a batch boundary with nothing on the GPU (device statistics equal to the counters) at least
+ * this often in a stream that never drains: see advance() */
+#define STATS_POINT_EVERY 32
 
 /* One batch: gathered, then launched (busy), then walked. */
 typedef struct {
@@ -65,12 +72,8 @@ typedef struct {
     int busy;              /* launched, not walked yet */
     uint64_t *desc;        /* pinned: offset << 16 | len */
     uint32_t *verdict;     /* pinned (mapped mode: written by the kernel over the link) */
-    uint8_t *win;          /* window mode: pinned header windows */
-    upe_hdr_rec_t *rec;    /* window mode: pinned records */
-    uint8_t *d_win;        /* window mode: device copies */
-    uint64_t *d_desc;
-    uint32_t *d_verdict;
-    upe_hdr_rec_t *d_rec;
+    uint8_t *win;          /* window mode: pinned header windows (read by the kernel there) */
+    upe_hdr_rec_t *rec;    /* pinned records (written by the kernel over the link) */
 } slot_t;
 
 typedef struct {
@@ -99,6 +102,7 @@ typedef struct {
                           rewrites the frames in the pool instead of emitting records */
     int prof;
     uint64_t t_wait, t_walk, t_launch, n_batches, t_flush;
+    unsigned since_point;  /* batches walked since the last publish with nothing in flight */
 } loop_t;
 
 static uint64_t mono_ns(void) {
@@ -188,14 +192,9 @@ static int launch(loop_t *L, int k) {
     } else if (L->pool) {
         rc = upe_gpu_process_mapped(L->ctx, L->pool, S->desc, S->verdict, n, NULL);
     } else {
-        rc = upe_gpu_memcpy_h2d(L->ctx, S->d_win, S->win, n * WIN, NULL);
-        if (rc == 0) rc = upe_gpu_memcpy_h2d(L->ctx, S->d_desc, S->desc, n * sizeof(uint64_t), NULL);
-        if (rc == 0)
-            rc = upe_gpu_process_emit(L->ctx, S->d_win, S->d_desc, S->d_verdict, S->d_rec, n, NULL);
-        if (rc == 0)
-            rc = upe_gpu_memcpy_d2h(L->ctx, S->verdict, S->d_verdict, n * sizeof(uint32_t), NULL);
-        if (rc == 0)
-            rc = upe_gpu_memcpy_d2h(L->ctx, S->rec, S->d_rec, n * sizeof(upe_hdr_rec_t), NULL);
+        /* the header windows in pinned staging, classified where they lie (the kernel reads them
+         * over the link, writes verdicts and records back): one launch, no DMA copies */
+        rc = upe_gpu_process_mapped_emit(L->ctx, S->win, S->desc, S->verdict, S->rec, n, NULL);
     }
     if (rc == 0) rc = upe_gpu_mark(L->ctx, k);
     S->busy = rc == 0;
@@ -233,20 +232,13 @@ static int walk(loop_t *L, int k) {
             if (code == UPE_V_FWD) rec_apply(d, &S->rec[rec++]);
         } else if (!L->pool) {
             /* window mode: the rewritten bytes into the caller's buffer (an answered ARP
-             * request ends a cut batch, so nothing is queued behind it: a synchronous copy) */
+             * request was rewritten by the kernel in its staged window) */
             if ((i & 63u) == 0) rec = i;
             if (code == UPE_V_FWD) {
                 rec_apply(d, &S->rec[rec++]);
             } else if (v & UPE_VF_ARP_REPLY) {
                 const size_t c = len < UPE_REWRITE_EXTENT ? len : UPE_REWRITE_EXTENT;
-                if (upe_gpu_memcpy_d2h(L->ctx, d, S->d_win + i * WIN, c, NULL) != 0 ||
-                    upe_gpu_sync(L->ctx, NULL) != 0) {
-                    /* the packets not walked yet stay held (for the drain) */
-                    memmove(S->bufs, S->bufs + i, (n - i) * sizeof(void *));
-                    S->n = n - i;
-                    S->busy = 0;
-                    return -1;
-                }
+                memcpy(d, S->win + i * WIN, c);
             }
         }
         if (L->left == 0) { /* the next burst starts here */
@@ -287,27 +279,50 @@ static int walk(loop_t *L, int k) {
         L->t_walk += t2 - t1;
     }
     if (cut && L->ops->load_neigh(L->user, L->ctx) != 0) return -1;
-    if (L->ops->publish) L->ops->publish(L->user, L->ctx, &L->c);
+    L->since_point++;
     return 0;
+}
+
+/* The counters so far to the program.  With a batch still on the GPU the context's statistics
+ * already hold some of its packets, which the counters do not: publish gets a NULL context then
+ * (counters only).  With nothing in flight it gets the context, whose upe_gpu_get_stats then
+ * matches the counters packet for packet. */
+static void publish(loop_t *L, int in_flight) {
+    if (!L->ops->publish) return;
+    L->ops->publish(L->user, in_flight ? NULL : L->ctx, &L->c);
+    if (!in_flight) L->since_point = 0;
 }
 
 /* Every batch held to completion, oldest first: the gathering slot's is launched first if it
  * holds packets.  Afterwards nothing is on the GPU. */
 static int finish_all(loop_t *L) {
     slot_t *G = &L->s[L->g];
+    const int any = G->n > 0 || L->o >= 0;
     if (G->n > 0 && !G->busy && launch(L, L->g) != 0) return -1;
     if (L->o >= 0 && walk(L, L->o) != 0) return -1;
     L->o = -1;
     if (G->busy && walk(L, L->g) != 0) return -1;
+    if (any) publish(L, 0);
     return 0;
 }
 
 /* The gathering slot is complete (full, or cut): launch it; walk the older batch meanwhile and
- * gather the next one into its slot — or, after a cut, drain everything. */
+ * gather the next one into its slot — or, after a cut, drain everything.  Every
+ * STATS_POINT_EVERY batches the older batch is walked BEFORE the launch instead, so that the
+ * program sees its statistics and counters agree at least that often (one batch's GPU time not
+ * hidden, once per STATS_POINT_EVERY). */
 static int advance(loop_t *L) {
     if (L->s[L->g].cut) return finish_all(L);
+    if (L->o >= 0 && L->since_point + 1 >= STATS_POINT_EVERY) {
+        if (walk(L, L->o) != 0) return -1;
+        L->o = -1;
+        publish(L, 0);
+    }
     if (launch(L, L->g) != 0) return -1;
-    if (L->o >= 0 && walk(L, L->o) != 0) return -1;
+    if (L->o >= 0) {
+        if (walk(L, L->o) != 0) return -1;
+        publish(L, 1);
+    }
     L->o = L->g;
     L->g = (L->g + 1) % NSLOT;
     return 0;
@@ -334,10 +349,6 @@ static void free_slots(loop_t *L) {
         if (S->verdict) upe_gpu_host_free(S->verdict);
         if (S->win) upe_gpu_host_free(S->win);
         if (S->rec) upe_gpu_host_free(S->rec);
-        if (S->d_win) upe_gpu_free(L->ctx, S->d_win);
-        if (S->d_desc) upe_gpu_free(L->ctx, S->d_desc);
-        if (S->d_verdict) upe_gpu_free(L->ctx, S->d_verdict);
-        if (S->d_rec) upe_gpu_free(L->ctx, S->d_rec);
     }
 }
 
@@ -356,17 +367,9 @@ static int alloc_slots(loop_t *L) {
         if (!L->pool) {
             S->win = upe_gpu_host_alloc(L->cap * WIN + UPE_FRAME_TAIL);
             S->rec = upe_gpu_host_alloc(L->cap * sizeof(upe_hdr_rec_t));
-            S->d_win = upe_gpu_malloc(L->ctx, L->cap * WIN + UPE_FRAME_TAIL);
-            S->d_desc = upe_gpu_malloc(L->ctx, L->cap * sizeof(uint64_t));
-            S->d_verdict = upe_gpu_malloc(L->ctx, L->cap * sizeof(uint32_t));
-            S->d_rec = upe_gpu_malloc(L->ctx, L->cap * sizeof(upe_hdr_rec_t));
-            if (!S->win || !S->rec || !S->d_win || !S->d_desc || !S->d_verdict || !S->d_rec)
-                return -1;
+            if (!S->win || !S->rec) return -1;
+            /* (the tail past the last window is read as zero by the kernel's window loads) */
             memset(S->win, 0, L->cap * WIN + UPE_FRAME_TAIL);
-            /* the tail past the last window (read as zero by the kernel's window loads) */
-            if (upe_gpu_memcpy_h2d(L->ctx, S->d_win + L->cap * WIN, S->win, UPE_FRAME_TAIL, NULL) ||
-                upe_gpu_sync(L->ctx, NULL))
-                return -1;
         }
     }
     return 0;
@@ -427,10 +430,17 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
             }
             /* the counters (and statistics) as they stand under the new state, even if no
              * batch follows for a while */
-            if (ops->publish) ops->publish(user, ctx, &L.c);
+            publish(&L, 0);
         }
         if (k == 0) {
-            if (G->n > 0 || L.o >= 0) { /* the ring is empty: classify what is held now */
+            /* the ring is empty: classify what is gathered now, keeping it in flight while the
+             * older batch is walked (a pool too small to fill a batch still overlaps), and walk
+             * the last batch in flight once the ring is still empty after that */
+            if (G->n > 0) {
+                if (advance(&L) != 0) goto fail;
+                continue;
+            }
+            if (L.o >= 0) {
                 if (finish_all(&L) != 0) goto fail;
                 continue;
             }
