@@ -369,6 +369,12 @@ typedef int (*upe_tx_batch_fn)(void *user, const uint8_t *const *frames, const s
 int upe_tx_flush(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t *h_verdict,
                  size_t n, size_t burst, upe_tx_batch_fn send, void *user, uint64_t *forwarded,
                  uint64_t *dropped);
+/* The same TX calls from the grouped egress list of upe_gpu_process_emit_tx (h_tx, h_tx_count
+ * copied to the host) instead of the verdicts: no per-packet verdict scan; the same calls,
+ * arguments and accounting as upe_tx_flush. */
+int upe_tx_flush_groups(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t *h_tx,
+                        const uint32_t *h_tx_count, size_t n, size_t burst, upe_tx_batch_fn send,
+                        void *user, uint64_t *forwarded, uint64_t *dropped);
 
 /* ------------------------------------------------------------------------------------------ */
 /* The GPU-backed worker loop (upe_amd/csrc/upe_worker.c, C)                                   */
@@ -523,6 +529,18 @@ int upe_gpu_process_rss(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d
  * (reference src/worker.c:240-243, 287-303).  Device buffers; d_index holds n entries. */
 int upe_gpu_compact(upe_gpu_ctx_t *ctx, const uint32_t *d_verdict, size_t n, uint32_t code,
                     uint32_t *d_index, uint64_t *d_count, void *stream);
+
+/* upe_gpu_process_emit() plus the egress list in the same pass, with no second kernel (round 6):
+ * the forwarded packets of group g (packets 64g .. 64g + 63) are d_tx[64g .. 64g + d_tx_count[g])
+ * in packet order — the order process_packet queues frames for tx_send_batch (reference
+ * src/worker.c:240-243, 287-303) — and d_tx[64g + k] is the packet whose record is d_hdr[64g + k]
+ * (the records' UPE_HDR_SLOT layout).  The groups concatenated are exactly upe_gpu_compact(...,
+ * UPE_V_FWD, ...)'s list; upe_tx_flush_groups() makes the reference worker's TX calls from it
+ * directly.  Device buffers: d_tx holds n entries, d_tx_count (n + 63) / 64; slots past a group's
+ * count are not written.  0 / -1. */
+int upe_gpu_process_emit_tx(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_desc,
+                            uint32_t *d_verdict, upe_hdr_rec_t *d_hdr, uint32_t *d_tx,
+                            uint32_t *d_tx_count, size_t n, void *stream);
 
 /* A batch with exact control-packet semantics, as the reference's burst loop runs it
  * (src/worker.c:23-104 inside process_packet): an ARP packet with the Ethernet/IPv4 header, or

@@ -76,3 +76,38 @@ def test_tx_burst_out_of_range(burst):
     wl, ref = golden_io.load("config_b_small")
     with pytest.raises(gpu.UpeGpuError, match="burst"):
         gpu.tx_flush(ref["frames"], wl.desc, ref["verdict"], burst)
+
+
+def grouped_list(verdict: np.ndarray):
+    """The egress list by 64-packet group that upe_gpu_process_emit_tx writes (include/upe_gpu.h):
+    group g's forwarded packets at tx[64g ..], their count in tx_count[g]; slots past a count left
+    as garbage (0xDEADBEEF here, to catch a reader that looks at them)."""
+    n = len(verdict)
+    fwd = (verdict & 0xF) == 4
+    tx = np.full(max(n, 1), 0xDEADBEEF, np.uint32)
+    cnt = np.zeros((n + 63) // 64, np.uint32)
+    for g in range(len(cnt)):
+        idx = np.nonzero(fwd[64 * g:64 * g + 64])[0] + 64 * g
+        tx[64 * g:64 * g + len(idx)] = idx
+        cnt[g] = len(idx)
+    return tx, cnt
+
+
+@pytest.mark.parametrize("burst", [32, 7, 64, 1])
+@pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_cf_small",
+                                  "config_d_small"])
+def test_tx_from_grouped_list_equals_reference(case, burst):
+    """upe_tx_flush_groups (the TX calls from the in-pass egress list) makes exactly the calls
+    upe_tx_flush makes from the verdicts; at the worker's burst of 32 those are the reference
+    worker's own tx_send_batch calls."""
+    wl, ref = golden_io.load(case)
+    v = ref["verdict"]
+    want = gpu.tx_flush(ref["frames"], wl.desc, v, burst)
+    got = gpu.tx_flush(ref["frames"], wl.desc, None, burst, groups=grouped_list(v))
+    assert [b[0].tolist() for b in got[0]] == [b[0].tolist() for b in want[0]]
+    assert [b[1] for b in got[0]] == [b[1] for b in want[0]]
+    assert got[1:] == want[1:]
+    if burst == WORKER_BURST_SIZE and oracle.ref_available():
+        oracle.run_reference(wl)
+        sizes, order = oracle.tx_log()
+        assert [len(b[0]) for b in got[0]] == sizes.tolist()

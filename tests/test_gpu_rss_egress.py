@@ -157,3 +157,56 @@ def test_mapped_batch_to_tx_batches(gpu_worker_factory, case):
     assert fwd == int(r.counters["pkts_forwarded"][0]) and drp == 0
     for x in (pf, pd, pv):
         x.free()
+
+
+@pytest.mark.parametrize("case", ["config_a", "config_b_small", "config_c_small",
+                                  "config_cf_small", "config_d_small"])
+def test_egress_list_in_the_classify_pass(gpu_worker_factory, case):
+    """upe_gpu_process_emit_tx: the classify pass itself leaves the forwarded packets by 64-packet
+    group (tx[64g ..], tx_count[g]) — concatenated, the REFERENCE worker's TX queue order
+    (src/worker.c:240-243) — with every record at the slot of its packet; the verdicts and
+    records equal plain emit mode's; and the TX calls made from it (upe_tx_flush_groups) are the
+    reference worker's own tx_send_batch calls."""
+    import oracle
+    from test_egress import WORKER_BURST_SIZE
+
+    wl, ref = golden_io.load(case)
+    n = wl.n
+    w = gpu_worker_factory(wl.capacity)
+    try:
+        w.configure(wl)
+        b = gpu.DeviceBatch(w, wl.frames, wl.desc)
+        b.hdr = w.malloc(max(16 * n, 16))
+        tx = w.malloc(max(4 * n, 4))
+        cnt = w.malloc(max(4 * ((n + 63) // 64), 4))
+        w.process_emit_tx(b.frames, b.desc, b.verdict, b.hdr, tx, cnt, n)
+        raw = b.fetch_hdr(raw=True)
+        _, v = b.fetch()
+        got_tx = np.zeros(max(n, 1), np.uint32)
+        got_cnt = np.zeros(max((n + 63) // 64, 1), np.uint32)
+        w.d2h(got_tx, tx)
+        w.d2h(got_cnt, cnt)
+        w.sync()
+        w.free(tx)
+        w.free(cnt)
+        b.free()
+    finally:
+        w.close()
+    assert np.array_equal(v, ref["verdict"])
+    fwd = np.nonzero((ref["verdict"] & 0xF) == V_FWD)[0]
+    lst = np.concatenate([got_tx[64 * g:64 * g + int(got_cnt[g])]
+                          for g in range((n + 63) // 64)]) if n else np.zeros(0, np.uint32)
+    assert np.array_equal(lst.astype(np.int64), fwd), "egress order differs from the reference's"
+    # each list slot holds the packet whose record is in that slot
+    rec = gpu.expand_records(raw, v)
+    for g in range((n + 63) // 64):
+        for k in range(int(got_cnt[g])):
+            assert np.array_equal(raw[64 * g + k], rec[got_tx[64 * g + k]])
+    if oracle.ref_available():
+        r = oracle.run_reference(wl)
+        sizes, order = oracle.tx_log()
+        batches, fw, dr = gpu.tx_flush(r.frames, wl.desc, None, WORKER_BURST_SIZE,
+                                       groups=(got_tx, got_cnt))
+        assert [len(x[0]) for x in batches] == sizes.tolist()
+        got = np.concatenate([x[0] for x in batches]) if batches else np.zeros(0, np.int64)
+        assert np.array_equal(got, order.astype(np.int64))

@@ -108,9 +108,6 @@ constexpr uint32_t kLateClaim = UPE_LATE_CLAIM;
 // the in-place one, bit 2 also the tuple-space ones (config B emit 26.2 -> 25.4 us per 1M batch;
 // C unchanged; in place +0.3 % with a VGPR spilled, so off; tuple space: D unchanged, with twice
 // the SGPR spills, so off; issued right after the parse instead: B no gain, C 39.0 -> 40.5).
-#ifndef UPE_TREE_MERGE
-#define UPE_TREE_MERGE 1   // tree_match: the five leaves' entries merged in list order (round 6)
-#endif
 #ifndef UPE_MID_PREFETCH
 #define UPE_MID_PREFETCH 1
 #endif
@@ -363,6 +360,8 @@ struct Args {
                                      // the verdicts (gb_packed: u32 keys, else u16 lengths)
     uint32_t gb_packed;              // 1: gb[i] = matched ? sorted rule index << 16 | len : 0
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
+    uint32_t* tx;                    // the egress-list kernels (kTx): group g's forwarded
+    uint32_t* tx_cnt;                // packets tx[64g .. 64g + tx_cnt[g])
     // this batch's slots of the between-batch state (DevState comment) follow from k6 = k % 6
     // (pointers computed where they are used: the kernel's scalar registers are scarce)
     uint32_t k6;
@@ -840,7 +839,6 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
     const uint4* g6 = a.fam + 2 * (size_t)a.fam4;
     uint32_t best = kNone, bact = 0;
     const bool fam_lds = (a.fam4_lds || a.fam4 == 0u) && (a.fam6_lds || a.fam6 == 0u);
-#if !UPE_TREE_MERGE
     // The leaf of one tree: its rules in list order until a match or a position >= best.
     auto leaf_tests = [&](const uint32_t lw) {
         const uint32_t cnt = lw >> 21, off = lw & 0x1FFFFFu;
@@ -911,85 +909,6 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             }
         }
     };
-#endif
-    // One leaf entry's rule against the key (the flagged covering entry matches without a test):
-    // its FamTable words from LDS (both lists staged: one address, the IPv6 words issued with the
-    // first two) or memory.
-    auto entry_matches = [&](const uint32_t p, const bool cov) -> bool {
-        if (fam_lds) {
-            const uint4* f = is6 ? l6 + kFamV6Stride * p : l4 + 2 * p;
-            const uint4 e0 = f[0], e1 = f[1];
-            uint32_t x6 = 0;
-            if (is6) {
-                const uint4 e2 = f[2], e3 = f[3], e4 = f[4];
-                x6 = ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
-                     ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
-            }
-            const uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
-                               ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w) | x6;
-            if (cov || x == 0u) bact = e0.z;
-            return cov || x == 0u;
-        }
-        uint4 e0, e1 = make_uint4(0, 0, 0, 0), e2 = e1, e3 = e1, e4 = e1;
-        if (is6) {
-            const uint4* f = a.fam6_lds ? l6 + kFamV6Stride * p : g6 + (size_t)kFamV6Stride * p;
-            e0 = f[0];
-            if (!cov) { e1 = f[1]; e2 = f[2]; e3 = f[3]; e4 = f[4]; }
-        } else {
-            const uint4* f = a.fam4_lds ? l4 + 2 * p : a.fam + 2 * (size_t)p;
-            e0 = f[0];
-            if (!cov) e1 = f[1];
-        }
-        uint32_t x = ((k0 ^ e0.x) & e0.y) | ((k1 ^ e0.z) & e0.w) |
-                     ((s[0] ^ e1.x) & e1.y) | ((d[0] ^ e1.z) & e1.w);
-        x |= ((s[1] ^ e2.x) & e2.w) | ((s[2] ^ e2.y) & e3.x) | ((s[3] ^ e2.z) & e3.y) |
-             ((d[1] ^ e3.z) & e4.y) | ((d[2] ^ e3.w) & e4.z) | ((d[3] ^ e4.x) & e4.w);
-        if (cov || x == 0u) bact = e0.z;
-        return cov || x == 0u;
-    };
-    // The five leaves merged (round 6): each leaf lists its rules in ascending list position and
-    // the trees' rules are disjoint, so taking the smallest next position over the five leaves
-    // visits a lane's candidates in list order, and the first that matches is the answer: no
-    // later entry of any leaf is read.  One loop for the wave (as long as its longest lane's
-    // merged prefix, not the sum over trees of each tree's longest leaf), and one dependent LDS
-    // round trip per step: the chosen leaf's next entry is read together with the rule words.
-    // A head is (position << 1 | covering flag), ~0 when the leaf is exhausted.
-    auto merged_tests = [&](const uint32_t (&lw)[kTreeFields]) {
-        // per leaf: its head, and (entries left after the head) << 21 | the next entry's index
-        uint32_t h[kTreeFields], c[kTreeFields];
-#pragma unroll
-        for (int t = 0; t < kTreeFields; ++t) {
-            const bool any = (lw[t] >> 21) != 0u;
-            h[t] = any ? __builtin_rotateleft32(E[lw[t] & 0x1FFFFFu], 1) : ~0u;
-            c[t] = any ? lw[t] + 1u - (1u << 21) : 0u;
-        }
-        bool look = active;
-        while (__any(look)) {
-            uint32_t m = h[0];
-#pragma unroll
-            for (int t = 1; t < kTreeFields; ++t) m = min(m, h[t]);
-            look = look && m != ~0u;
-            if (look) {
-                // the chosen leaf moves on: its next entry is loaded with the rule words
-                uint32_t cc = 0u;
-#pragma unroll
-                for (int t = 0; t < kTreeFields; ++t) cc = h[t] == m ? c[t] : cc;
-                const uint32_t nxe = (cc >> 21) != 0u
-                                         ? __builtin_rotateleft32(E[cc & 0x1FFFFFu], 1) : ~0u;
-                const uint32_t p = m >> 1;
-                if (entry_matches(p, (m & 1u) != 0u)) {
-                    best = p;
-                    look = false;
-                }
-#pragma unroll
-                for (int t = 0; t < kTreeFields; ++t) {
-                    const bool sel = h[t] == m;
-                    h[t] = sel ? nxe : h[t];
-                    c[t] = sel ? cc + 1u - (1u << 21) : c[t];
-                }
-            }
-        }
-    };
     // an address tree's key word for a dimension: one of its field's words (big-endian for IPv6
     // where the image says so, so that a prefix is a range; IPv4's host-order word 0 and zeros),
     // or a port or the protocol (dimensions 8-10); bit selects keep them in registers
@@ -1037,23 +956,10 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
             step(qb, ib, lb, vb, [&](uint32_t dm) { return addr_word(dm, wd); });
             step(qc, ic, lc, vc, [&](uint32_t) { return dp; });
         }
-#if UPE_TREE_MERGE
-        uint32_t ja = first + 2u, jb = first + 4u, ma = 0, mb = 0;
-        bool wa = nt != 0u, wb = wa;
-        while (__any(wa || wb)) {
-            const uint4 qa = S[ja], qb = S[jb];
-            step(qa, ja, ma, wa, [&](uint32_t) { return sp; });
-            step(qb, jb, mb, wb, [&](uint32_t) { return pr; });
-        }
-        const uint32_t lw[kTreeFields] = {la, lb, lc, ma, mb};
-        merged_tests(lw);
-#else
         leaf_tests(la);
         leaf_tests(lb);
         leaf_tests(lc);
-#endif
     }
-#if !UPE_TREE_MERGE
     {
         uint32_t ia = first + 2u, ib = first + 4u, la = 0, lb = 0;
         bool va = nt != 0u, vb = va;
@@ -1065,7 +971,6 @@ __device__ __forceinline__ uint32_t tree_match(const Args& a, bool active, bool 
         leaf_tests(la);
         leaf_tests(lb);
     }
-#endif
     if (__any(active && best == kNone)) {
         // no tree's rule: the family's rule that matches every key, if it has one
         const uint2 dflt = N[1];
@@ -1586,6 +1491,8 @@ __device__ void census_probe(uint32_t* w, uint32_t grid) {
 // the tables (agreement then holds until the host changes the tables or the L1 state) or whose
 // family's index is empty; the look-back is not compiled in, and an entry that disagrees with an
 // empty index answers its candidates itself (no packet can hit that table first).
+// kRing && kHost (emit only): the egress-list kernels (kTx, upe_gpu_process_emit_tx) — that bit
+// pair is otherwise unused (a ring is never a host launch), so the list costs no variant bit.
 // kRing (lean emit only): a ring launch — a batch of a.ring_cpb chunks completes when every
 // workgroup owning part of it has finished its chunks of it; the last one stamps the time.
 template <bool kTssMode, bool kEmit, bool kLean = false, bool kNoLB = false, bool kRing = false,
@@ -1595,6 +1502,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     // carries another flavour's code): 0 small table from its LDS copy, 1 family lists, 2 whole
     // table through the scalar unit, 3 decision tree over the family lists
     constexpr bool kFam = kScan == 1, kGlb = kScan == 2, kTree = kScan == 3;
+    constexpr bool kTx = kRing && kHost;          // the egress list (see above), not a ring
+    constexpr bool kRingL = kRing && !kHost;      // a ring launch
     constexpr bool kFamIdx = kFam || kTree;   // the match is a FamTable index-array entry
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[]; // [nrules_pad][2]
     // per wave: 8 counters, first f4 / f6 / ctrl, last m4 / m6
@@ -1604,7 +1513,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
     __shared__ u32x8 s_rv4[kTssMode || kScan ? 1 : kSmallRules];   // small tables: RuleV4 / RuleV6
     __shared__ u32x16 s_rv6[kTssMode || kScan ? 1 : kSmallRules];  // words (only kScan 0 has them)
     __shared__ uint32_t s_claim;   // the workgroup's next unclaimed chunk (workgroup-local index)
-    __shared__ uint32_t s_bdone[kRing ? kRingMax : 1];   // ring: the workgroup's chunks done per batch
+    __shared__ uint32_t s_bdone[kRingL ? kRingMax : 1];   // ring: the workgroup's chunks done per batch
 
     if (a.census) {
         if (threadIdx.x == 0) census_probe(a.st->census, gridDim.x);
@@ -1675,9 +1584,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         return t < a.ntiles && c * 64u < a.n ? c : kNone;
     };
     if (tid == 0) s_claim = kWaves;
-    if (kRing)
+    if (kRingL)
         for (uint32_t k = tid; k < (uint32_t)kRingMax; k += kBlock) s_bdone[k] = 0u;
-    if (kRing && tid == 0)   // the ring's time origin: the first workgroup to start
+    if (kRingL && tid == 0)   // the ring's time origin: the first workgroup to start
         __hip_atomic_fetch_min(a.ring_t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < C_N + 3) s_tot[tid] = tid < C_N ? 0u : kNone;
@@ -2122,6 +2031,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
         if (live)   // written through (sc1): no dirty lines left for the boundary
             __hip_atomic_store(&a.verdict[i], code | flags | rbits, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        // the egress list in the same pass (upe_gpu_process_emit_tx): each forwarded packet's
+        // index in its record's slot, and the group's count (src/worker.c:240-243 queues the
+        // forwarded frames in packet order).  Its own kernel instantiations (kTx), so that no
+        // other launch carries the code or its registers.
+        if (kTx) {
+            const unsigned long long fm = __ballot(live && code == UPE_V_FWD);
+            if (live && code == UPE_V_FWD)
+                a.tx[ch * 64u + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = i;
+            if (lane == 0) a.tx_cnt[ch] = (uint32_t)__popcll(fm);
+        }
         // the side array upe_rule_hist reads (lean linear-scan launches never have it; the
         // tuple-space tables it serves always do)
         if ((kTssMode || !kLean) && a.gb && live) {
@@ -2185,7 +2105,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
                 s_pay[wave][6] = r.d[3]; s_pay[wave][7] = mlo; s_pay[wave][8] = mhi;
             }
         }
-        if (kRing) {
+        if (kRingL) {
             // every workgroup owns ring_mine chunks of each batch (the host launches the ring
             // kernel only when a batch's tiles divide evenly over the grid, and for at most
             // kRingMax batches: one LDS counter per batch, however far apart the workgroup's
@@ -2962,17 +2882,19 @@ hipStream_t pick(upe_gpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->strea
 constexpr int kVarCount = 256;
 // Kernel variants: bit 0 emit, bit 1 tuple space, bit 2 lean, bit 3 no look-back (lean only),
 // bit 4 ring (lean emit linear scan only), bit 5 a host path's launch (upe_gpu_process_mapped /
-// upe_gpu_process_host; not ring), bits 6-7 how a linear-scan table past kSmallRules is matched
+// upe_gpu_process_host; not ring), bits 4 and 5 together the egress-list kernels (emit, device
+// batches; upe_gpu_process_emit_tx), bits 6-7 how a linear-scan table past kSmallRules is matched
 // (never with tuple space): 1 its family lists (FamTable), 2 the whole table through the scalar
 // unit, 3 the decision tree over the family lists.
 enum { VAR_EMIT = 1, VAR_TSS = 2, VAR_LEAN = 4, VAR_NOLB = 8, VAR_RING = 16, VAR_HOST = 32,
        VAR_FAM = 64, VAR_GLB = 128, VAR_TREE = 192, VAR_SCAN = 192 };
 // scan: 0 small table (LDS copy), 1 family lists, 2 whole table through the scalar unit, 3 tree
 int classify_var(bool tss, bool emit, bool lean, bool nolb, bool ring = false, bool host = false,
-                 int scan = 0) {
+                 int scan = 0, bool tx = false) {
     return (!tss ? (scan & 3) * VAR_FAM : 0) |
-           (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0) | (lean && nolb ? VAR_NOLB : 0) |
-           (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) | (emit ? VAR_EMIT : 0);
+           (tx ? VAR_RING | VAR_HOST : (host && !ring ? VAR_HOST : 0) | (ring ? VAR_RING : 0)) |
+           (lean && nolb ? VAR_NOLB : 0) | (lean ? VAR_LEAN : 0) | (tss ? VAR_TSS : 0) |
+           (emit ? VAR_EMIT : 0);
 }
 // The instantiated variants (every combination classify_var can return for a launch).
 constexpr bool var_built(int v) {
@@ -2980,7 +2902,8 @@ constexpr bool var_built(int v) {
                host = v & VAR_HOST;
     if (nolb && !lean) return false;
     if ((v & VAR_SCAN) && (v & VAR_TSS)) return false;
-    if (ring) return !host && emit && lean && !(v & VAR_TSS);
+    if (ring && host) return emit;   // the egress-list kernels
+    if (ring) return emit && lean && !(v & VAR_TSS);
     return true;
 }
 template <int V>
@@ -4589,7 +4512,8 @@ struct RingReq {
 };
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
-                 const RingReq* ring = nullptr, bool host = false) {
+                 const RingReq* ring = nullptr, bool host = false, uint32_t* d_tx = nullptr,
+                 uint32_t* d_tx_cnt = nullptr) {
     if (!c) return fail("null context");
     host = host || c->host_tag;
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
@@ -4604,7 +4528,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             const size_t m = n - s0 < kMaxLaunch ? n - s0 : kMaxLaunch;
             if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
                              d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
-                             m, stream, nullptr, host) != 0)
+                             m, stream, nullptr, host, d_tx ? d_tx + s0 : nullptr,
+                             d_tx_cnt ? d_tx_cnt + s0 / 64 : nullptr) != 0)
                 return -1;
         }
         return 0;
@@ -4636,6 +4561,8 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.desc = d_desc;
     a.verdict = d_verdict;
     a.n = (uint32_t)n;
+    a.tx = d_tx;
+    a.tx_cnt = d_tx_cnt;
     a.rv4 = c->rv4;
     a.rv6 = c->rv6;
     a.fam = c->fam;
@@ -4752,14 +4679,16 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     // a ring launch stamps its batches' completion with the ring kernels (lean emit linear scan)
     // (at most kRingMax batches: one LDS counter each)
     bool stamp = ring && ring->done && emit && lean && !c->tss && n / ring->per <= (size_t)kRingMax;
-    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, scan);
+    const bool tx = d_tx != nullptr;   // (emit, device batches: upe_gpu_process_emit_tx)
+    if (tx) stamp = host = false;
+    int var = classify_var(c->tss, emit, lean, c->no_lb, stamp, host, scan, tx);
     // persistent grid: the workgroups the chip holds at once (or one per tile if fewer)
     uint32_t grid_cap = resident_grid(c, var, lds, s);
     if (grid_cap == 0) return -1;
     // the census of the no-look-back counterpart now as well, so that the switch to it (a few
     // launches later) does not put a synchronous census launch in the middle of a batch stream
     if (lean && !c->no_lb &&
-        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host, scan), lds, s) == 0)
+        resident_grid(c, classify_var(c->tss, emit, true, true, stamp, host, scan, tx), lds, s) == 0)
         return -1;
     // Tiles of kWaves chunks (one per wave of a workgroup); a batch too small to give every
     // resident workgroup a tile gets narrower tiles, down to one chunk, so that it spreads over
@@ -4875,6 +4804,14 @@ int upe_gpu_process_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_
                          uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, size_t n, void* stream) {
     if (n && !d_hdr) return fail("null header records");
     return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream);
+}
+
+int upe_gpu_process_emit_tx(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,
+                            uint32_t* d_verdict, upe_hdr_rec_t* d_hdr, uint32_t* d_tx,
+                            uint32_t* d_tx_count, size_t n, void* stream) {
+    if (n && (!d_hdr || !d_tx || !d_tx_count)) return fail("null header records or egress list");
+    return process_impl(c, d_frames, d_desc, d_verdict, nullptr, d_hdr, n, stream, nullptr, false,
+                        d_tx, d_tx_count);
 }
 
 int upe_gpu_process_ring_emit(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc,

@@ -364,3 +364,37 @@ int upe_tx_flush(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t
     }
     return 0;
 }
+
+int upe_tx_flush_groups(const uint8_t *h_frames, const uint64_t *h_desc, const uint32_t *h_tx,
+                        const uint32_t *h_tx_count, size_t n, size_t burst, upe_tx_batch_fn send,
+                        void *user, uint64_t *forwarded, uint64_t *dropped) {
+    if (burst == 0 || burst > UPE_TX_BATCH_MAX)
+        return host_fail("upe_tx_flush_groups: burst %d must be 1..UPE_TX_BATCH_MAX", (int)burst, "");
+    if (n && (!h_frames || !h_desc || !h_tx || !h_tx_count || !send))
+        return host_fail("upe_tx_flush_groups: null argument%.0d%s", 0, "");
+    const uint8_t *frames[UPE_TX_BATCH_MAX];
+    size_t lens[UPE_TX_BATCH_MAX];
+    size_t g = 0, k = 0; /* the next list entry: group g, its k-th forwarded packet */
+    for (size_t base = 0; base < n; base += burst) {
+        const size_t end = n - base < burst ? n : base + burst;
+        int count = 0;
+        for (;;) {
+            if (g * 64 >= end || g * 64 >= n) break;
+            const uint32_t cnt = h_tx_count[g];
+            if (cnt > 64) return host_fail("upe_tx_flush_groups: group count %d above 64", (int)cnt, "");
+            if (k >= cnt) { g++; k = 0; continue; }
+            const uint32_t i = h_tx[g * 64 + k];
+            if (i >= end) break; /* the next burst's */
+            frames[count] = h_frames + (h_desc[i] >> 16);
+            lens[count++] = (size_t)(h_desc[i] & 0xFFFFu);
+            k++;
+        }
+        if (count == 0) continue; /* src/worker.c:287: no call for an all-dropped burst */
+        int sent = send(user, frames, lens, count);
+        if (sent < 0) sent = 0;
+        if (sent > count) sent = count;
+        if (forwarded) *forwarded += (uint64_t)sent;
+        if (dropped) *dropped += (uint64_t)(count - sent);
+    }
+    return 0;
+}

@@ -122,6 +122,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_compact": (I, [P, P, SZ, ctypes.c_uint32, P, P, P]),
         "upe_gpu_process_segmented": (I, [P, P, P, P, SZ, P, SZ, P, SZ, ctypes.c_int64, P, P]),
         "upe_gpu_process_emit": (I, [P, P, P, P, P, SZ, P]),
+        "upe_gpu_process_emit_tx": (I, [P, P, P, P, P, P, P, SZ, P]),
         "upe_gpu_process_batches_emit": (I, [P, P, P, P, P, SZ, SZ, P]),
         "upe_gpu_process_ring_emit": (I, [P, P, P, P, P, SZ, SZ, P, P]),
         "upe_gpu_process_queue_emit": (I, [P, P, SZ, P]),
@@ -133,6 +134,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_mapped": (I, [P, P, P, P, SZ, P]),
         "upe_gpu_process_mapped_emit": (I, [P, P, P, P, P, SZ, P]),
         "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
+        "upe_tx_flush_groups": (I, [P, P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
         "upe_gpu_worker_run": (I, [P, ctypes.POINTER(WorkerOps), P, ctypes.POINTER(WorkerCfg),
                                    P]),
     }
@@ -173,7 +175,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
-            "upe_tx_flush",
+            "upe_tx_flush", "upe_tx_flush_groups", "upe_gpu_process_emit_tx",
             "upe_gpu_worker_run")
 
 
@@ -398,6 +400,14 @@ class GpuWorker:
             len(ndp), now, ctypes.byref(nw), stream or None), "upe_gpu_process_segmented")
         return nw.value
 
+    def process_emit_tx(self, frames, desc, verdict, hdr, tx, tx_count, n: int,
+                        stream=None) -> None:
+        """upe_gpu_process_emit plus the egress list by 64-packet group (device buffers)."""
+        _check(LIB.upe_gpu_process_emit_tx(self._ctx, _dev_ptr(frames), _dev_ptr(desc),
+                                           _dev_ptr(verdict), _dev_ptr(hdr), _dev_ptr(tx),
+                                           _dev_ptr(tx_count), n, stream or None),
+               "upe_gpu_process_emit_tx")
+
     def compact(self, verdict, n: int, code: int, index, count, stream=None) -> None:
         """Indexes of the packets with verdict code `code`, in packet order (device buffers)."""
         _check(LIB.upe_gpu_compact(self._ctx, _dev_ptr(verdict), n, code, _dev_ptr(index),
@@ -554,13 +564,14 @@ class PinnedArray:
 
 
 def tx_flush(frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray, burst: int = 32,
-             sent_of=None):
+             sent_of=None, groups=None):
     """upe_tx_flush over a host batch: returns (batches, forwarded, dropped), batches = one
     (packet indexes, frame bytes) pair per TX call in call order.  sent_of(count) -> frames the
-    stand-in for sendmmsg reports sent (default: all)."""
+    stand-in for sendmmsg reports sent (default: all).  groups = (tx, tx_count): the grouped
+    egress list of upe_gpu_process_emit_tx instead of the verdicts (upe_tx_flush_groups)."""
     frames = np.ascontiguousarray(frames)
     desc = np.ascontiguousarray(desc, dtype=np.uint64)
-    verdict = np.ascontiguousarray(verdict, dtype=np.uint32)
+    verdict = None if verdict is None else np.ascontiguousarray(verdict, dtype=np.uint32)
     base = frames.ctypes.data
     index_of = {int(o): i for i, o in enumerate((desc >> np.uint64(16)).tolist())}
     batches = []
@@ -577,8 +588,16 @@ def tx_flush(frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray, burst: i
     fn = TX_BATCH_FN(cb)
     fwd = ctypes.c_uint64(0)
     drp = ctypes.c_uint64(0)
-    rc = LIB.upe_tx_flush(_np_ptr(frames), _np_ptr(desc), _np_ptr(verdict), int(desc.shape[0]),
-                          int(burst), fn, None, ctypes.byref(fwd), ctypes.byref(drp))
+    if groups is not None:
+        tx = np.ascontiguousarray(groups[0], dtype=np.uint32)
+        cnt = np.ascontiguousarray(groups[1], dtype=np.uint32)
+        rc = LIB.upe_tx_flush_groups(_np_ptr(frames), _np_ptr(desc), _np_ptr(tx), _np_ptr(cnt),
+                                     int(desc.shape[0]), int(burst), fn, None, ctypes.byref(fwd),
+                                     ctypes.byref(drp))
+    else:
+        rc = LIB.upe_tx_flush(_np_ptr(frames), _np_ptr(desc), _np_ptr(verdict),
+                              int(desc.shape[0]), int(burst), fn, None, ctypes.byref(fwd),
+                              ctypes.byref(drp))
     if rc != 0:
         raise UpeGpuError(f"upe_tx_flush: {LIB.upe_host_last_error().decode()}")
     return batches, int(fwd.value), int(drp.value)
