@@ -735,6 +735,32 @@ def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
                     "not value (value = one launch per batch)"}
 
 
+def line_summary(out: dict) -> dict:
+    """The line's headline figures in one small object, printed last (a reader that keeps only the
+    tail of a long line still sees them): per leg Mpps, kernel time, roofline fraction and
+    counted bytes per packet; the CPU baseline; the host-inclusive rates."""
+    def leg(d):
+        if not d:
+            return None
+        r = d.get("roofline", {})
+        k = r.get("kernel_ms", r.get("classify_ms"))
+        t = r.get("traffic")
+        n = d.get("packets_per_gpu_step") or (out["config"]["packets_per_gpu_step"]
+                                               if d is out else None)
+        return {"mpps": d.get("value"), "kernel_us": round(k * 1e3, 2) if k else None,
+                "frac": r.get("frac"),
+                "counted_B_per_packet": round(t / n, 1) if t and n else r.get("traffic_bytes_per_packet"),
+                "algorithmic_B_per_packet": r.get("algorithmic_bytes_per_packet")}
+    cb = out.get("cpu_baseline") or {}
+    return {"B": leg(out), "imix_CF": leg(out.get("imix")), "C3": leg(out.get("imix_seed3")),
+            "C6": leg(out.get("imix_v6fwd")), "D": leg(out.get("config_d")),
+            "ring_us_per_batch": (out.get("ring") or {}).get("us_per_batch"),
+            "host_mapped_emit_mpps": (out.get("host_mapped_emit") or {}).get("value"),
+            "host_roundtrip_mpps": (out.get("host_roundtrip") or {}).get("value"),
+            "cpu_baseline_mpps": cb.get("value"), "cpu_cores": cb.get("cores"),
+            "n_gpus": out.get("n_gpus"), "lib_sha16": out.get("lib_sha16")}
+
+
 def launch_cmd(gpus: int, argv: list, port: int) -> list:
     """The command the parent runs for --gpus N > 1 without a launcher around it: N ranks on
     this node under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1), each
@@ -1167,6 +1193,7 @@ def main() -> None:
                 dp = dropin_pipeline(local_cpus, args.dropin_seconds, local)
                 if dp:
                     out["dropin_pipeline"] = dp
+        out["summary"] = line_summary(out)   # last: what a truncated tail of the line still shows
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier(group=host_group)
