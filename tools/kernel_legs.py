@@ -61,7 +61,10 @@ def main() -> None:
             d = [(e - s) / 1e3 for s, e in seg]
             cut = a.min_frac * statistics.median(d)
             full = [x for x in d if x >= cut]
-            print(f"{name[:100]:100s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
+            short = name
+            if "upe_classify<" in name:   # the instantiation's template arguments
+                short = "upe_classify<" + name.split("upe_classify<", 1)[1].split(">", 1)[0] + ">"
+            print(f"{short[:100]:100s} {i:3d} {len(d):6d} {statistics.mean(d):9.2f} "
                   f"{min(d):9.2f} {max(d):9.2f} {len(d) - len(full):6d} {len(full):6d} "
                   f"{statistics.mean(full):12.2f} {min(full):11.2f}")
 
