@@ -278,8 +278,16 @@ int upe_gpu_process(upe_gpu_ctx_t *ctx, uint8_t *d_frames, const uint64_t *d_des
  * group in packet order — forwarded packet i's record is rec[64 * (i / 64) + k], k = the number
  * of forwarded packets before it among packets 64 * (i / 64) .. i - 1 (the kernel's ballot and
  * lane count; a reader walking the verdicts in order keeps a cursor, reset to i at every multiple
- * of 64).  The other slots are not written.  UPE_HDR_SLOT gives the slot from that count. */
+ * of 64).  The other slots are not written.  UPE_HDR_SLOT gives the slot from that count.
+ *
+ * BREAKING CHANGE in layout 2 (round 5): layout 1 (rounds 1-4) wrote one record per packet at
+ * rec[i], zero for packets not forwarded.  A caller that reads rec[i] per packet applies wrong or
+ * stale records under layout 2 without any error: it must walk with the cursor above (or
+ * UPE_HDR_SLOT), or check UPE_HDR_LAYOUT at compile time and upe_gpu_hdr_layout() at run time
+ * (the library it actually loaded) before trusting either form. */
+#define UPE_HDR_LAYOUT 2
 #define UPE_HDR_SLOT(i, k) ((((size_t)(i)) & ~(size_t)63) + (size_t)(k))
+int upe_gpu_hdr_layout(void);   /* UPE_HDR_LAYOUT of the loaded library */
 typedef struct {
     uint8_t b[16];
 } upe_hdr_rec_t;

@@ -135,3 +135,13 @@ def test_verdict_helpers():
     d = layout.make_desc(np.array([0, 64]), np.array([64, 1518]))
     assert layout.desc_offsets(d).tolist() == [0, 64]
     assert layout.desc_lens(d).tolist() == [64, 1518]
+
+
+def test_record_layout_version():
+    """the emit-mode record layout changed in round 5 (records compacted per 64-packet
+    group); the header names the layout and the library reports the one it was built with."""
+    from upe_amd import gpu
+
+    m = re.search(r"#define UPE_HDR_LAYOUT (\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == 2
+    assert gpu.LIB.upe_gpu_hdr_layout() == 2

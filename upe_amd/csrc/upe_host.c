@@ -398,3 +398,5 @@ int upe_tx_flush_groups(const uint8_t *h_frames, const uint64_t *h_desc, const u
     }
     return 0;
 }
+
+int upe_gpu_hdr_layout(void) { return UPE_HDR_LAYOUT; }

@@ -135,6 +135,7 @@ def _load() -> ctypes.CDLL:
         "upe_gpu_process_mapped_emit": (I, [P, P, P, P, P, SZ, P]),
         "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
         "upe_tx_flush_groups": (I, [P, P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
+        "upe_gpu_hdr_layout": (I, []),
         "upe_gpu_worker_run": (I, [P, ctypes.POINTER(WorkerOps), P, ctypes.POINTER(WorkerCfg),
                                    P]),
     }
@@ -175,7 +176,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_host_last_error",
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
-            "upe_tx_flush", "upe_tx_flush_groups", "upe_gpu_process_emit_tx",
+            "upe_tx_flush", "upe_tx_flush_groups", "upe_gpu_process_emit_tx", "upe_gpu_hdr_layout",
             "upe_gpu_worker_run")
 
 
