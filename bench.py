@@ -684,6 +684,61 @@ def config_d_leg(torch, dev, local: int, steps: int, warmup: int, copies_cap: in
                     "cycled; emit mode"}
 
 
+def egress_leg(torch, dev, wl, worker, pool, stride: int, copies: int, desc, launches: int = 20) -> dict:
+    """The egress list (not `value`): the same batches as `value` classified by
+    upe_gpu_process_emit (no list), by upe_gpu_process_emit_tx (the list of forwarded packets by
+    64-packet group written in the same pass) and by upe_gpu_process_emit followed by
+    upe_gpu_compact (the flat list from the verdicts: two more kernels).  HIP events on the launch
+    stream around each mode's `launches` launches; per-launch time.  The list of the last launch
+    is checked against the verdicts (the flat list equals the groups concatenated)."""
+    from upe_amd.layout import V_FWD
+
+    n = wl.n
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    tx = torch.empty(n, dtype=torch.int32, device=dev)
+    txc = torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)
+    idx = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    base = pool.data_ptr()
+
+    def run(mode: str, k: int) -> None:
+        f = base + (k % copies) * stride
+        if mode == "emit_tx":
+            worker.process_emit_tx(f, desc, verdict, hdr, tx, txc, n, sh)
+        else:
+            worker.process_emit(f, desc, verdict, hdr, n, sh)
+            if mode == "emit+compact":
+                worker.compact(verdict, n, V_FWD, idx, cnt, sh)
+
+    out = {}
+    for mode in ("emit", "emit_tx", "emit+compact", "emit"):
+        for k in range(3):
+            run(mode, k)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record()
+        for k in range(launches):
+            run(mode, 3 + k)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        us = e0.elapsed_time(e1) * 1e3 / launches
+        out[mode] = round(min(us, out.get(mode, us)), 3)
+    v = verdict.cpu().numpy().view(np.uint32)
+    fwd = np.nonzero((v & 0xF) == V_FWD)[0]
+    t, c = tx.cpu().numpy().view(np.uint32), txc.cpu().numpy().view(np.uint32)
+    groups = np.concatenate([t[64 * g:64 * g + int(c[g])] for g in range(len(c))])
+    flat = idx.cpu().numpy().view(np.uint32)[: int(cnt.item())]
+    ok = bool(np.array_equal(groups, fwd) and np.array_equal(flat, fwd))
+    del verdict, hdr, tx, txc, idx, cnt
+    return {"us_per_launch": out, "lists_equal_verdicts": ok, "launches": launches,
+            "what": "per launch over the value leg's batches (HIP events on the launch stream, the "
+                    "lower of two passes for emit): emit alone, emit with the egress list by "
+                    "64-packet group in the same pass (upe_gpu_process_emit_tx), emit + the flat "
+                    "list by upe_gpu_compact (two more kernels over the verdicts)"}
+
+
 def ring_leg(torch, dev, dist, wl, worker, count: int, launches: int) -> dict:
     """Ring mode (upe_gpu_process_ring_emit, not `value`): `count` batches of this workload, each
     its own copy of the frames, laid out back to back and classified by ONE launch; the launch's
@@ -755,6 +810,7 @@ def line_summary(out: dict) -> dict:
     return {"B": leg(out), "imix_CF": leg(out.get("imix")), "C3": leg(out.get("imix_seed3")),
             "C6": leg(out.get("imix_v6fwd")), "D": leg(out.get("config_d")),
             "ring_us_per_batch": (out.get("ring") or {}).get("us_per_batch"),
+            "egress_us_per_launch": (out.get("egress") or {}).get("us_per_launch"),
             "host_mapped_emit_mpps": (out.get("host_mapped_emit") or {}).get("value"),
             "host_roundtrip_mpps": (out.get("host_roundtrip") or {}).get("value"),
             "cpu_baseline_mpps": cb.get("value"), "cpu_cores": cb.get("cores"),
@@ -1012,6 +1068,9 @@ def main() -> None:
     if args.config == "B" and args.strong and not args.packets:
         strong = {k: strong_leg(torch, dev, dist, rank, world, local, k, args.steps, args.warmup)
                   for k in ("B", "C")}
+    egress = None
+    if args.config == "B" and args.mode == "emit" and not args.packets and rank == 0:
+        egress = egress_leg(torch, dev, wl, worker, pool, stride, copies, desc)
     ring = None
     if args.config == "B" and args.ring > 0 and not args.packets:
         ring = ring_leg(torch, dev, dist, wl, worker, args.ring, 12)
@@ -1129,6 +1188,8 @@ def main() -> None:
             out["strong"] = strong
         if ring:
             out["ring"] = ring
+        if egress:
+            out["egress"] = egress
         if dleg:
             out["config_d"] = dleg
         if shared:

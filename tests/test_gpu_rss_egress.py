@@ -210,3 +210,48 @@ def test_egress_list_in_the_classify_pass(gpu_worker_factory, case):
         assert [len(x[0]) for x in batches] == sizes.tolist()
         got = np.concatenate([x[0] for x in batches]) if batches else np.zeros(0, np.int64)
         assert np.array_equal(got, order.astype(np.int64))
+
+
+@pytest.mark.parametrize("make", [lambda: synth.config_b(n=1 << 20, seed=2),
+                                  lambda: synth.config_c_flows(n=1 << 20, seed=3)],
+                         ids=["B_1M", "CF_1M"])
+def test_egress_list_in_pass_full_size(gpu_worker_factory, make):
+    """At full size (1M packets, the bench's B and the IMIX headline CF): the in-pass egress list
+    concatenated equals upe_gpu_compact's flat FWD list from the same launch's verdicts, and the
+    verdicts and records equal a plain emit launch's."""
+    import torch
+
+    wl = make()
+    n = wl.n
+    dev = torch.device("cuda", 0)
+    fr = torch.from_numpy(wl.frames).to(dev)
+    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
+    out = {}
+    for mode in ("emit", "emit_tx"):
+        w = gpu_worker_factory(wl.capacity)
+        try:
+            w.configure(wl)
+            v = torch.empty(n, dtype=torch.int32, device=dev)
+            hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+            if mode == "emit":
+                w.process_emit(fr, desc, v, hdr, n)
+                idx = torch.empty(n, dtype=torch.int32, device=dev)
+                cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+                w.compact(v, n, V_FWD, idx, cnt)
+                w.sync()
+                out["flat"] = idx.cpu().numpy().view(np.uint32)[: int(cnt.item())]
+            else:
+                tx = torch.empty(n, dtype=torch.int32, device=dev)
+                tc = torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)
+                w.process_emit_tx(fr, desc, v, hdr, tx, tc, n)
+                w.sync()
+                t, c = tx.cpu().numpy().view(np.uint32), tc.cpu().numpy().view(np.uint32)
+                out["groups"] = np.concatenate([t[64 * g:64 * g + int(c[g])]
+                                                for g in range(len(c))])
+            vv = v.cpu().numpy().view(np.uint32)
+            out[mode] = (vv, gpu.expand_records(hdr.cpu().numpy().reshape(n, 16), vv))
+        finally:
+            w.close()
+    assert np.array_equal(out["emit"][0], out["emit_tx"][0])
+    assert np.array_equal(out["emit"][1], out["emit_tx"][1])
+    assert out["flat"].size > 0 and np.array_equal(out["groups"], out["flat"])
