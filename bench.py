@@ -694,7 +694,10 @@ def egress_leg(torch, dev, wl, worker, pool, stride: int, copies: int, desc, lau
     from upe_amd.layout import V_FWD
 
     n = wl.n
-    sh = torch.cuda.current_stream(dev).cuda_stream
+    # a stream of our own, so that the events below bracket exactly these launches (torch's
+    # current stream is the null stream, which the library maps to the context's own stream)
+    strm = torch.cuda.Stream(dev)
+    sh = strm.cuda_stream
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     tx = torch.empty(n, dtype=torch.int32, device=dev)
@@ -713,15 +716,16 @@ def egress_leg(torch, dev, wl, worker, pool, stride: int, copies: int, desc, lau
                 worker.compact(verdict, n, V_FWD, idx, cnt, sh)
 
     out = {}
+    torch.cuda.synchronize(dev)
     for mode in ("emit", "emit_tx", "emit+compact", "emit"):
         for k in range(3):
             run(mode, k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(dev)
-        e0.record()
+        e0.record(strm)
         for k in range(launches):
             run(mode, 3 + k)
-        e1.record()
+        e1.record(strm)
         torch.cuda.synchronize(dev)
         us = e0.elapsed_time(e1) * 1e3 / launches
         out[mode] = round(min(us, out.get(mode, us)), 3)

@@ -219,37 +219,45 @@ def test_egress_list_in_pass_full_size(gpu_worker_factory, make):
     """At full size (1M packets, the bench's B and the IMIX headline CF): the in-pass egress list
     concatenated equals upe_gpu_compact's flat FWD list from the same launch's verdicts, and the
     verdicts and records equal a plain emit launch's."""
-    import torch
-
     wl = make()
     n = wl.n
-    dev = torch.device("cuda", 0)
-    fr = torch.from_numpy(wl.frames).to(dev)
-    desc = torch.from_numpy(wl.desc.view(np.int64)).to(dev)
     out = {}
     for mode in ("emit", "emit_tx"):
         w = gpu_worker_factory(wl.capacity)
         try:
             w.configure(wl)
-            v = torch.empty(n, dtype=torch.int32, device=dev)
-            hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+            b = gpu.DeviceBatch(w, wl.frames, wl.desc)
+            b.hdr = w.malloc(16 * n)
             if mode == "emit":
-                w.process_emit(fr, desc, v, hdr, n)
-                idx = torch.empty(n, dtype=torch.int32, device=dev)
-                cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-                w.compact(v, n, V_FWD, idx, cnt)
+                b.run_emit()
+                idx, cnt = w.malloc(4 * n), w.malloc(8)
+                w.compact(b.verdict, n, V_FWD, idx, cnt)
+                k = np.zeros(1, np.uint64)
+                w.d2h(k, cnt)
                 w.sync()
-                out["flat"] = idx.cpu().numpy().view(np.uint32)[: int(cnt.item())]
+                flat = np.zeros(max(int(k[0]), 1), np.uint32)
+                w.d2h(flat, idx)
+                w.sync()
+                out["flat"] = flat[: int(k[0])]
+                w.free(idx)
+                w.free(cnt)
             else:
-                tx = torch.empty(n, dtype=torch.int32, device=dev)
-                tc = torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)
-                w.process_emit_tx(fr, desc, v, hdr, tx, tc, n)
+                tx, tc = w.malloc(4 * n), w.malloc(4 * ((n + 63) // 64))
+                w.process_emit_tx(b.frames, b.desc, b.verdict, b.hdr, tx, tc, n)
+                t = np.zeros(n, np.uint32)
+                c = np.zeros((n + 63) // 64, np.uint32)
                 w.sync()
-                t, c = tx.cpu().numpy().view(np.uint32), tc.cpu().numpy().view(np.uint32)
+                w.d2h(t, tx)
+                w.d2h(c, tc)
+                w.sync()
                 out["groups"] = np.concatenate([t[64 * g:64 * g + int(c[g])]
                                                 for g in range(len(c))])
-            vv = v.cpu().numpy().view(np.uint32)
-            out[mode] = (vv, gpu.expand_records(hdr.cpu().numpy().reshape(n, 16), vv))
+                w.free(tx)
+                w.free(tc)
+            rec = b.fetch_hdr()
+            _, v = b.fetch()
+            out[mode] = (v, rec)
+            b.free()
         finally:
             w.close()
     assert np.array_equal(out["emit"][0], out["emit_tx"][0])
