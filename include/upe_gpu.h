@@ -214,6 +214,22 @@ int upe_gpu_load_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count
 int upe_gpu_reload_rules(upe_gpu_ctx_t *ctx, const upe_rule_t *rules, size_t count,
                          size_t rule_capacity, upe_rule_stat_t *old_stats, size_t old_capacity);
 
+/* The same reload in two halves (round 6), so that the table is built where the reference
+ * builds it — in the stats thread, before the swap, while the workers keep forwarding
+ * (src/main.c:222-257) — and the worker thread only uploads it between two bursts.
+ * upe_rules_compile: the compiled table (rule words, family lists, tuple-space index or decision
+ * tree) of `count` sorted rules for a rule_stats of rule_capacity entries; host only (no
+ * context, no GPU), any thread; NULL on error (upe_gpu_last_error() on the calling thread).  The
+ * build is what dominates a reload of a large table: 0.4 ms (1k rules, scanned) to ~300 ms
+ * (16k flow rules, decision tree) on the GPU box's host.
+ * upe_gpu_reload_image: upe_gpu_reload_rules() with that image (the capacity is the image's);
+ * the image is not consumed.  upe_rules_image_free: NULL is a no-op. */
+typedef struct upe_rule_image upe_rule_image_t;
+upe_rule_image_t *upe_rules_compile(const upe_rule_t *rules, size_t count, size_t rule_capacity);
+int upe_gpu_reload_image(upe_gpu_ctx_t *ctx, const upe_rule_image_t *image,
+                         upe_rule_stat_t *old_stats, size_t old_capacity);
+void upe_rules_image_free(upe_rule_image_t *image);
+
 /* How the loaded table is classified: 0 = linear first-match scan (tables of up to 64 rules, or
  * a table whose tree outgrew its node budget), 1 = tuple-space index (large tables whose rules
  * fall into few mask signatures: one hash probe per signature, visited in order of each

@@ -83,6 +83,10 @@ typedef struct {
     uint64_t stats_last_ns;
     upe_counters_t counters;        /* the loop's, at the end */
     uint64_t consumed;              /* published: NS / NA consumed (no worker_t field) */
+    /* the stats thread's precompiled image of the next table (upe_rules_compile) and the table
+     * it belongs to, stored before the swap (round 6): the worker thread then only uploads it */
+    const rule_table_t *image_rt;
+    upe_rule_image_t *image;
     int rc;
 } gpu_worker_t;
 
@@ -128,7 +132,10 @@ static int op_sync(void *u, upe_gpu_ctx_t *ctx) {
     const rule_table_t *rt = __atomic_load_n(&GW(u)->w->rt, __ATOMIC_ACQUIRE);
     GW(u)->rt_loaded = rt;
     GW(u)->stats_loaded = __atomic_load_n(&GW(u)->w->rule_stats, __ATOMIC_ACQUIRE);
-    /* old rule_stats are not handed back: the stats thread frees the old array */
+    /* old rule_stats are not handed back: the stats thread frees the old array.  The table's
+     * image, when the stats thread compiled it before the swap (stored before rt: acquire) */
+    if (__atomic_load_n(&GW(u)->image_rt, __ATOMIC_ACQUIRE) == rt && GW(u)->image)
+        return upe_gpu_reload_image(ctx, GW(u)->image, NULL, 0);
     return upe_gpu_reload_rules(ctx, (const upe_rule_t *)rt->rules, rt->count, rt->capacity, NULL, 0);
 }
 static void op_publish(void *u, upe_gpu_ctx_t *ctx, const upe_counters_t *c) {
@@ -380,6 +387,10 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
             if (rule_table_add(rt_b, (const rule_t *)&rules_b[i]) != 0) return -1;
         rule_stat_t *new_stats = calloc(rt_b->capacity, sizeof(rule_stat_t));
         if (!new_stats) return -1;
+        /* the GPU worker's image of the new table, built here on the stats thread while the
+         * worker keeps forwarding (NULL: the worker compiles it at the swap instead) */
+        g.image = upe_rules_compile((const upe_rule_t *)rt_b->rules, rt_b->count, rt_b->capacity);
+        __atomic_store_n(&g.image_rt, rt_b, __ATOMIC_RELEASE);
         old_stats = w->rule_stats;
         memcpy(stats_a, old_stats, capacity * sizeof(rule_stat_t));
         __atomic_store_n(&w->rule_stats, new_stats, __ATOMIC_RELEASE);
@@ -391,6 +402,7 @@ int upe_dropin_run(const upe_rule_t *rules, size_t nrules, size_t capacity,
     }
     g_stop = 1;
     pthread_join(th, NULL);
+    upe_rules_image_free(g.image);
     counters[0] = w->pkts_in;
     counters[1] = w->pkts_parsed;
     counters[2] = w->pkts_matched;

@@ -21,14 +21,21 @@ from upe_amd import gpu, synth
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_reload(w, wl, rules_b_sorted, cap_b, at, emit, sync_before):
+def _gpu_reload(w, wl, rules_b_sorted, cap_b, at, emit, sync_before, image=False):
     """Batch [0, at) with the loaded table, reload, batch [at, n); the reload is issued while
-    the first batch may still be running unless sync_before."""
+    the first batch may still be running unless sync_before.  image: the new table compiled
+    beforehand (upe_rules_compile, while the first batch runs) and installed by
+    upe_gpu_reload_image."""
     b1 = gpu.DeviceBatch(w, wl.frames, wl.desc[:at])
     (b1.run_emit if emit else b1.run)()
     if sync_before:
         w.sync()
-    old = w.reload_rules(rules_b_sorted, cap_b)
+    if image:
+        im = gpu.RuleImage(rules_b_sorted, cap_b)
+        old = w.reload_image(im)
+        im.free()
+    else:
+        old = w.reload_rules(rules_b_sorted, cap_b)
     frames1, v1 = b1.fetch()
     if emit:
         frames1 = gpu.hdr_apply(frames1, wl.desc[:at], b1.fetch_hdr())
@@ -43,16 +50,17 @@ def _gpu_reload(w, wl, rules_b_sorted, cap_b, at, emit, sync_before):
     return frames, np.concatenate([v1, v2]), counters, stats, w.get_l1(), old
 
 
+@pytest.mark.parametrize("image", [False, True], ids=["rules", "image"])
 @pytest.mark.parametrize("emit", [False, True])
 @pytest.mark.parametrize("name", ["B", "C", "D"])
-def test_reload_equals_reference(gpu_worker_factory, name, emit):
+def test_reload_equals_reference(gpu_worker_factory, name, emit, image):
     wl, rules_b, at, cap_b = reload_util.case(name)
     ref, old_ref = oracle.run_reference_reload(wl, rules_b, cap_b, at)
     w = gpu_worker_factory(wl.capacity)
     try:
         w.configure(wl)
         frames, verdict, counters, stats, l1, old = _gpu_reload(
-            w, wl, ref.rules_sorted, cap_b, at, emit, sync_before=name == "C")
+            w, wl, ref.rules_sorted, cap_b, at, emit, sync_before=name == "C", image=image)
         assert w.capacity == cap_b and stats.shape[0] == cap_b
     finally:
         w.close()

@@ -129,3 +129,25 @@ def test_pcap_rejects_bad_files(tmp_path):
     p.write_bytes(data[:-10])             # truncated record
     with pytest.raises(gpu.UpeGpuError):
         gpu.pcap_read(str(p))
+
+
+def test_rule_image_compiles_without_a_gpu():
+    """upe_rules_compile builds the table on the host alone (no context, no GPU: the stats thread
+    can do it while the workers forward), for every index kind; bad arguments fail cleanly."""
+    from upe_amd import gpu, synth
+
+    for wl in (synth.config_b(n=64), synth.config_c_flows(n=64), synth.config_d(n=64)):
+        im = gpu.RuleImage(wl.rules_sorted, wl.capacity)
+        assert im.ptr
+        im.free()
+        im.free()   # idempotent
+    wl = synth.config_b(n=64)
+    with pytest.raises(gpu.UpeGpuError, match="capacity"):
+        gpu.RuleImage(wl.rules_sorted, 0)
+    with pytest.raises(gpu.UpeGpuError, match="exceeds the capacity"):
+        gpu.RuleImage(wl.rules_sorted, 2)   # more rules than rule_stats entries
+    r = wl.rules_sorted.copy()
+    r["rule_id"][0] = 1000
+    with pytest.raises(gpu.UpeGpuError, match="rule_id"):
+        gpu.RuleImage(r, len(r))            # a rule id past the rule_stats
+    gpu.LIB.upe_rules_image_free(None)

@@ -4014,21 +4014,44 @@ void replace(T*& field, DevBuf& b) {
     field = b.take<T>();
 }
 
-// upe_gpu_load_rules, and upe_gpu_reload_rules with `fresh` (a zeroed rule_stats of fresh_cap
-// entries that replaces the context's, the old per-index totals dropped instead of credited).
-// Everything the new table needs is built and uploaded before the context changes: on an error
-// the context keeps classifying with the old table and its statistics.
-int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
-                    DevBuf* fresh, size_t fresh_cap) {
-    const size_t cap = fresh ? fresh_cap : c->cap;
-    const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
+}  // namespace
+
+// The compiled table a context classifies with (round 6: built apart from any context, so that
+// a program's stats thread can build it while the workers keep forwarding, as the reference's
+// does before its SIGHUP swap, src/main.c:222-257): the rule words, the family lists, the
+// tuple-space index or the decision tree, and the flags the launches need.  Host memory only.
+struct upe_rule_image {
+    size_t count = 0, cap = 0, pad = 0;
     std::vector<RuleV4> v4;
     std::vector<RuleV6> v6;
     std::vector<int2> info;
+    bool fwd4 = false, fwd6 = false;
+    uint32_t fam4 = 0, fam6 = 0, fam_all = 0, fam_x1idx = 0;
+    std::vector<uint4> fimg;
+    bool tss = false;
+    TssFamily f4, f6;
+    std::vector<uint16_t> fps;
+    bool tree_ok = false;
+    std::vector<uint4> timg;
+    TreeImage t;
+};
+
+namespace {
+// Compile a sorted table of `count` rules for a context whose rule_stats hold `cap` entries
+// (host only: no context, no GPU; any thread).  0, or -1 (upe_gpu_last_error()).
+int build_image(const upe_rule_t* rules, size_t count, size_t cap, upe_rule_image& im) {
+    im.count = count;
+    im.cap = cap;
+    const size_t pad = ((count + kUnroll - 1) / kUnroll + 1) * kUnroll;  // >= 1 padding block
+    im.pad = pad;
+    std::vector<RuleV4>& v4 = im.v4;
+    std::vector<RuleV6>& v6 = im.v6;
+    std::vector<int2>& info = im.info;
     if (compile_rules(rules, count, cap, pad, v4, v6, info) != 0) return -1;
     // a family none of whose reachable rules forwards never consults or updates its L1 entry
     // (src/worker.c:155-244 run only for forwarded packets): its entry's agreement is moot
-    bool fwd4 = false, fwd6 = false;
+    bool& fwd4 = im.fwd4;
+    bool& fwd6 = im.fwd6;
     {
         bool e4 = false, e6 = false;
         for (size_t i = 0; i < count && !(e4 && e6); ++i) {
@@ -4040,9 +4063,12 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
         }
     }
     // linear-scan tables past the LDS copy: the per-family lists (FamTable)
-    uint32_t fam4 = 0, fam6 = 0, fam_all = 0, fam_x1idx = 0;
+    uint32_t& fam4 = im.fam4;
+    uint32_t& fam6 = im.fam6;
+    uint32_t& fam_all = im.fam_all;
+    uint32_t& fam_x1idx = im.fam_x1idx;
     std::vector<uint32_t> l4, l6;   // the family lists' sorted indexes
-    std::vector<uint4> fimg;
+    std::vector<uint4>& fimg = im.fimg;
     if (pad > (size_t)kSmallRules) {
         bool end4 = false, end6 = false;
         family_lists(rules, count, v4, v6, l4, l6, end4, end6);
@@ -4083,9 +4109,10 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
     }
     // Large tables: a tuple-space index when the rules fall into few mask signatures (one hash
     // probe per signature instead of a test per rule).
-    bool tss = false;
-    TssFamily f4, f6;
-    std::vector<uint16_t> fps;   // the staged fingerprint image
+    bool& tss = im.tss;
+    TssFamily& f4 = im.f4;
+    TssFamily& f6 = im.f6;
+    std::vector<uint16_t>& fps = im.fps;   // the staged fingerprint image
     const char* force = getenv("UPE_GPU_TSS");   // diagnostic: 0 = never, 1 = always
     if (count > 0 && count < kTssMaxRules && !(force && force[0] == '0') &&
         build_tss_family(4, v4, v6, rules, count, f4) && build_tss_family(6, v4, v6, rules, count, f6)) {
@@ -4112,9 +4139,9 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
     // scan's cost is then bounded by that, and its wave-uniform scalar loads beat the walk:
     // seed-3 config C 38.1 vs 46.5 us).  UPE_GPU_TREE: 0 = never, 1 = whenever it builds
     // (diagnostics); UPE_GPU_TREE_BINTH: rules per leaf before a split.
-    bool tree_ok = false;
-    std::vector<uint4> timg;
-    TreeImage t;
+    bool& tree_ok = im.tree_ok;
+    std::vector<uint4>& timg = im.timg;
+    TreeImage& t = im.t;
     const char* tf = getenv("UPE_GPU_TREE");
     // (the reach first, from the lists alone: a table a scan never walks far into is not built a
     // tree only to throw it away — ADVICE r05; a reload then costs the lists, not the forest)
@@ -4136,7 +4163,28 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
             tree_ok = reach > kTreeMinReach || (tf && tf[0] == '1');
         }
     }
+    return 0;
+}
 
+// upe_gpu_load_rules / upe_gpu_reload_rules[_image] with a compiled image: `fresh` (a zeroed
+// rule_stats of fresh_cap entries) replaces the context's statistics on a reload, the old
+// per-index totals dropped instead of credited.  Everything the new table needs is uploaded
+// before the context changes: on an error the context keeps classifying with the old table and
+// its statistics.
+int install_image(upe_gpu_ctx_t* c, const upe_rule_image& im, DevBuf* fresh, size_t fresh_cap) {
+    const size_t count = im.count, pad = im.pad;
+    const std::vector<RuleV4>& v4 = im.v4;
+    const std::vector<RuleV6>& v6 = im.v6;
+    const std::vector<int2>& info = im.info;
+    const std::vector<uint4>& fimg = im.fimg;
+    const bool tss = im.tss, tree_ok = im.tree_ok;
+    const TssFamily& f4 = im.f4;
+    const TssFamily& f6 = im.f6;
+    const std::vector<uint16_t>& fps = im.fps;
+    const std::vector<uint4>& timg = im.timg;
+    const TreeImage& t = im.t;
+    const uint32_t fam4 = im.fam4, fam6 = im.fam6, fam_all = im.fam_all, fam_x1idx = im.fam_x1idx;
+    const bool fwd4 = im.fwd4, fwd6 = im.fwd6;
     // every image on the device before anything of the context changes
     DevBuf b_rv4, b_rv6, b_rinfo, b_idx, b_fam, b_tfs, b_tg4, b_tg6, b_tt4, b_tt6, b_tree;
     if (b_rv4.put(v4.data(), pad * sizeof(RuleV4)) || b_rv6.put(v6.data(), pad * sizeof(RuleV6)) ||
@@ -4215,6 +4263,13 @@ int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
                            : upe_rule_index_info_t{};
     return publish(c);   // the DevState's pointers (stats, stats_idx)
 }
+
+int load_rules_impl(upe_gpu_ctx_t* c, const upe_rule_t* rules, size_t count,
+                    DevBuf* fresh, size_t fresh_cap) {
+    upe_rule_image im;
+    if (build_image(rules, count, fresh ? fresh_cap : c->cap, im) != 0) return -1;
+    return install_image(c, im, fresh, fresh_cap);
+}
 }  // namespace
 
 extern "C" {
@@ -4255,6 +4310,45 @@ extern "C" int upe_gpu_reload_rules(upe_gpu_ctx_t* c, const upe_rule_t* rules, s
     HIP_TRY(hipMalloc(&fresh.p, rule_capacity * 2 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(fresh.p, 0, rule_capacity * 2 * sizeof(unsigned long long)));
     return load_rules_impl(c, rules, count, &fresh, rule_capacity);
+}
+
+extern "C" upe_rule_image_t* upe_rules_compile(const upe_rule_t* rules, size_t count,
+                                               size_t rule_capacity) {
+    if (rule_capacity == 0 || rule_capacity > (1u << 24)) {
+        fail("rule_capacity must be in [1, 2^24]");
+        return nullptr;
+    }
+    if (count > rule_capacity || (count && !rules)) {
+        fail(count > rule_capacity ? "rule count exceeds the capacity" : "null rules");
+        return nullptr;
+    }
+    try {
+        auto* im = new upe_rule_image;
+        if (build_image(rules, count, rule_capacity, *im) != 0) {
+            delete im;
+            return nullptr;
+        }
+        return im;
+    } catch (const std::bad_alloc&) {
+        fail("out of memory (rule image)");
+        return nullptr;
+    }
+}
+
+extern "C" void upe_rules_image_free(upe_rule_image_t* im) { delete im; }
+
+extern "C" int upe_gpu_reload_image(upe_gpu_ctx_t* c, const upe_rule_image_t* im,
+                                    upe_rule_stat_t* old_stats, size_t old_capacity) {
+    if (!c || !im) return fail("null context or image");
+    if (old_capacity && !old_stats) return fail("null old_stats");
+    DEV_SCOPE(c->device);
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (old_capacity && read_rule_stats(c, old_stats, old_capacity) != 0) return -1;
+    DevBuf fresh;
+    HIP_TRY(hipMalloc(&fresh.p, im->cap * 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(fresh.p, 0, im->cap * 2 * sizeof(unsigned long long)));
+    return install_image(c, *im, &fresh, im->cap);
 }
 
 // (not part of the ABI; upe_worker.c) tag this context's launches as a host-side loop's: they

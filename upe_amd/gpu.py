@@ -136,6 +136,9 @@ def _load() -> ctypes.CDLL:
         "upe_tx_flush": (I, [P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
         "upe_tx_flush_groups": (I, [P, P, P, P, SZ, SZ, TX_BATCH_FN, P, P, P]),
         "upe_gpu_hdr_layout": (I, []),
+        "upe_rules_compile": (P, [P, SZ, SZ]),
+        "upe_gpu_reload_image": (I, [P, P, P, SZ]),
+        "upe_rules_image_free": (None, [P]),
         "upe_gpu_worker_run": (I, [P, ctypes.POINTER(WorkerOps), P, ctypes.POINTER(WorkerCfg),
                                    P]),
     }
@@ -177,6 +180,7 @@ EXPORTED = ("upe_gpu_last_error", "upe_gpu_device_count", "upe_gpu_local_cpus", 
             "upe_gpu_host_alloc", "upe_gpu_host_free", "upe_gpu_host_register",
             "upe_gpu_host_unregister", "upe_gpu_process_mapped", "upe_gpu_process_mapped_emit",
             "upe_tx_flush", "upe_tx_flush_groups", "upe_gpu_process_emit_tx", "upe_gpu_hdr_layout",
+            "upe_rules_compile", "upe_gpu_reload_image", "upe_rules_image_free",
             "upe_gpu_worker_run")
 
 
@@ -267,6 +271,15 @@ class GpuWorker:
                                         self.capacity if want_old else 0),
                "upe_gpu_reload_rules")
         self.capacity = cap
+        return old
+
+    def reload_image(self, image: "RuleImage", want_old: bool = True):
+        """upe_gpu_reload_image: reload_rules with a table compiled beforehand (RuleImage, e.g. on
+        another thread); the capacity is the image's.  Returns the old rule_stats when want_old."""
+        old = np.zeros(self.capacity, RULE_STAT_DTYPE) if want_old else None
+        _check(LIB.upe_gpu_reload_image(self._ctx, image.ptr, _np_ptr(old) if want_old else None,
+                                        self.capacity if want_old else 0), "upe_gpu_reload_image")
+        self.capacity = image.capacity
         return old
 
     def rule_index_kind(self) -> int:
@@ -602,6 +615,27 @@ def tx_flush(frames: np.ndarray, desc: np.ndarray, verdict: np.ndarray, burst: i
     if rc != 0:
         raise UpeGpuError(f"upe_tx_flush: {LIB.upe_host_last_error().decode()}")
     return batches, int(fwd.value), int(drp.value)
+
+
+class RuleImage:
+    """upe_rules_compile: a sorted rule table compiled for the GPU path on the host, with no
+    context or GPU (the reference's stats thread builds its new table before the swap the same
+    way, src/main.c:222-257); free() (or garbage collection) releases it."""
+
+    def __init__(self, rules_sorted: np.ndarray, capacity: int):
+        r = np.ascontiguousarray(rules_sorted, dtype=RULE_DTYPE)
+        self.capacity = int(capacity)
+        self.ptr = LIB.upe_rules_compile(_np_ptr(r) if len(r) else None, len(r), self.capacity)
+        if not self.ptr:
+            raise UpeGpuError(LIB.upe_gpu_last_error().decode())
+
+    def free(self) -> None:
+        if self.ptr:
+            LIB.upe_rules_image_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
 
 
 class RegisteredArray:
