@@ -271,10 +271,7 @@ struct __attribute__((aligned(16))) TssGroup {
 // hold v = (index + 1) | action << 22 (0 = empty slot), so a probe is one 16-byte load, one
 // memory request (two loads into one line were two requests: tools/fetch_calib), and the IPv4
 // slot array takes half the L2 (config D 755 -> 716 us per 16M against 32-byte slots).
-#ifndef UPE_TSS_SLOT6
-#define UPE_TSS_SLOT6 3
-#endif
-constexpr int kTssSlot4 = 1, kTssSlot6 = UPE_TSS_SLOT6;   // uint4 per slot
+constexpr int kTssSlot4 = 1, kTssSlot6 = 3;   // uint4 per slot
 constexpr uint32_t kTssMaxRules = 1u << 22;   // index + 1 in 22 bits, the action above it
 // Fingerprints of small groups staged in LDS (word [15] of such a group: 1 + its offset in the
 // staged image): their probes then wait for no fingerprint round trip.
