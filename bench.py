@@ -477,7 +477,7 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
                                        for k in range(warmup, warmup + steps)])
     run(0, warmup)
     torch.cuda.synchronize(dev)
-    worker.timing_span(EVENT_EVERY, EVENT_SPAN)
+    worker.timing_span(event_every(steps), EVENT_SPAN)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -495,7 +495,8 @@ def imix_leg(torch, dev, dist, rank: int, local: int, steps: int, warmup: int, m
     worker.close()
     del pool, desc, verdict, hdr
     bpp = algorithmic_bytes(wl, v, emit=mode == "emit")
-    kern_s = cms / launches / 1e3 if launches else float("nan")
+    # (no closed event sample: the wall time per step, an upper bound on the kernel's)
+    kern_s = cms / launches / 1e3 if launches else elapsed / steps
     achieved = float(bpp.sum()) / kern_s / 1e9
     return {"workload": WORKLOADS[kind], "value": round(total / elapsed / 1e6, 2), "unit": "Mpps",
             "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps,
@@ -821,6 +822,37 @@ def line_summary(out: dict) -> dict:
             "n_gpus": out.get("n_gpus"), "lib_sha16": out.get("lib_sha16")}
 
 
+def finite(x):
+    """The line as strict JSON: a NaN or infinity (a leg that could not be timed) becomes null."""
+    if isinstance(x, float):
+        return x if x == x and abs(x) != float("inf") else None
+    if isinstance(x, dict):
+        return {k: finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [finite(v) for v in x]
+    return x
+
+
+class stdout_to_stderr:
+    """File descriptor 1 points at stderr inside the block (C++ libraries write there too)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def event_every(steps: int) -> int:
+    """Timing samples (EVENT_SPAN launches each) every this many steps: EVENT_EVERY, or fewer
+    for a short run so that at least one sample closes inside it."""
+    return EVENT_EVERY if steps >= 2 * EVENT_EVERY else max(1, steps // 2)
+
+
 def launch_cmd(gpus: int, argv: list, port: int) -> list:
     """The command the parent runs for --gpus N > 1 without a launcher around it: N ranks on
     this node under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1), each
@@ -929,14 +961,17 @@ def main() -> None:
         # RCCL ("nccl") carries only the barrier and the max / sum over ranks; the gloo backend
         # (UPE_BENCH_DIST_BACKEND=gloo) rehearses the multi-rank path on a one-GPU box
         backend = os.environ.get("UPE_BENCH_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-        # a host-side group for the wait while rank 0 times the CPU baseline (no GPU spin)
         import datetime
 
-        host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
+        # (gloo prints its connection lines on stdout, which carries only the JSON line: they go
+        # to stderr while the groups are made)
+        with stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+            # a host-side group for the wait while rank 0 times the CPU baseline (no GPU spin)
+            host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
     else:
         torch.cuda.set_device(local)
 
@@ -1008,7 +1043,7 @@ def main() -> None:
     # 5 launches the pair's latency is spread thin (the gaps between those launches remain in
     # the time).  UPE_BENCH_EVENTS=0: diagnostic run without them.
     events = os.environ.get("UPE_BENCH_EVENTS", "1") != "0"
-    worker.timing_span(EVENT_EVERY if events else 0, EVENT_SPAN)
+    worker.timing_span(event_every(args.steps) if events else 0, EVENT_SPAN)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -1042,7 +1077,7 @@ def main() -> None:
     if not args.no_other_mode:
         om = "inplace" if args.mode == "emit" else "emit"
         steps(0, min(args.warmup, 5), om)
-        worker.timing_span(EVENT_EVERY if events else 0, EVENT_SPAN)
+        worker.timing_span(event_every(args.steps) if events else 0, EVENT_SPAN)
         torch.cuda.synchronize(dev)
         ta = time.perf_counter()
         steps(args.warmup, args.steps, om)
@@ -1126,7 +1161,10 @@ def main() -> None:
         bytes_per_launch = float(bpp.sum())
         # a step's kernels: the classify launch plus (tables over 4096 rules) the rule_stats
         # group-by; finalize_ms is the group-by's share (0 for smaller tables)
-        kern_s = (classify_ms + finalize_ms) / launches / 1e3 if launches else float("nan")
+        # (no closed event sample, e.g. UPE_BENCH_EVENTS=0: the wall time per step, an upper
+        # bound on the kernels')
+        kern_s = ((classify_ms + finalize_ms) / launches / 1e3 if launches
+                  else elapsed / args.steps)
         achieved = bytes_per_launch / kern_s / 1e9
         ms_step = elapsed / args.steps * 1e3
         out = {
@@ -1259,7 +1297,7 @@ def main() -> None:
                 if dp:
                     out["dropin_pipeline"] = dp
         out["summary"] = line_summary(out)   # last: what a truncated tail of the line still shows
-        print(json.dumps(out), flush=True)
+        print(json.dumps(finite(out)), flush=True)
     if dist:
         dist.barrier(group=host_group)
     worker.close()

@@ -112,8 +112,9 @@ def test_bench_two_ranks():
            "--imix-v6fwd", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    # stdout carries the JSON line and nothing else (gloo's connection lines go to stderr)
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["value"] > 0 and d["imix"]["value"] > 0
