@@ -3,7 +3,8 @@ oracle, bit-exact on verdict words, rewritten frames, counters, rule_stats and L
 
 Sizes: the golden fixtures (reference outputs, tests/golden/) at small sizes; BASELINE.json's
 full sizes against reference digests (B 1M, C 1M, D 256k x 64k rules) and, for D at 16M,
-size-independent properties plus a random-chunk comparison against the oracle.
+size-independent properties, a random-chunk comparison against the oracle and every packet
+classified by two independent indexes (tuple space, decision tree) that must agree.
 """
 from __future__ import annotations
 
@@ -331,6 +332,32 @@ def test_config_d_full_properties(gpu_worker_factory, emit):
         v = verdict[start:start + 4096]
         # verdict code, rule index and the TTL/checksum rewrite do not depend on L1 history
         assert np.array_equal(v & 0xFFFFFF0F, r.verdict & 0xFFFFFF0F)
+
+
+def test_config_d_full_two_indexes_agree(gpu_worker_factory, monkeypatch):
+    """16M packets x 64k rules, every packet: the tuple-space index (D's default) and the
+    decision tree over the family lists (forced, image read from memory) are two independent
+    first-match classifiers of the same table (src/rule_table.c:163-176); each is pinned to the
+    reference on the fixtures (test_rule_index_kinds_agree).  Over the whole batch they must give
+    the same verdict word, rewritten bytes, counters, rule_stats and L1 state — a size-independent
+    check of every packet the random-chunk comparison above does not reach."""
+    wl = synth.config_d()
+    got = {}
+    for mode in ("tss", "tree"):
+        monkeypatch.setenv("UPE_GPU_TSS", "1" if mode == "tss" else "0")
+        monkeypatch.setenv("UPE_GPU_TREE", "1")
+        w = gpu_worker_factory(wl.capacity)
+        try:
+            w.configure(wl)
+            assert w.rule_index_kind() == (1 if mode == "tss" else 2)
+            got[mode] = gpu.run_workload(wl, worker=w, emit=True)
+        finally:
+            w.close()
+    frames, verdict, counters, stats, l1 = got["tree"]
+    _assert_same(got["tss"], {"verdict": verdict, "frames": frames, "counters": counters,
+                              "rule_stats": stats, "l1": l1}, "D 16M tuple space vs tree")
+    codes = np.bincount(verdict & 0xF, minlength=7)
+    assert codes[V_FWD] > 0 and int(counters[0]["pkts_in"]) == wl.n
 
 
 @pytest.mark.parametrize("emit", [False, True])
