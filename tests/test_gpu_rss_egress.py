@@ -213,12 +213,14 @@ def test_egress_list_in_the_classify_pass(gpu_worker_factory, case):
 
 
 @pytest.mark.parametrize("make", [lambda: synth.config_b(n=1 << 20, seed=2),
-                                  lambda: synth.config_c_flows(n=1 << 20, seed=3)],
-                         ids=["B_1M", "CF_1M"])
+                                  lambda: synth.config_c_flows(n=1 << 20, seed=3),
+                                  lambda: synth.config_b(n=(1 << 24) + 4096 + 37, seed=5)],
+                         ids=["B_1M", "CF_1M", "B_past_2^24"])
 def test_egress_list_in_pass_full_size(gpu_worker_factory, make):
     """At full size (1M packets, the bench's B and the IMIX headline CF): the in-pass egress list
     concatenated equals upe_gpu_compact's flat FWD list from the same launch's verdicts, and the
-    verdicts and records equal a plain emit launch's."""
+    verdicts and records equal a plain emit launch's.  Past 2^24 packets the batch runs as
+    several launches, and the list still holds indexes into the caller's whole batch."""
     wl = make()
     n = wl.n
     out = {}

@@ -362,6 +362,8 @@ struct Args {
     uint4* hdr;                      // emit mode: [n] rewritten-header records (upe_hdr_rec_t)
     uint32_t* tx;                    // the egress-list kernels (kTx): group g's forwarded
     uint32_t* tx_cnt;                // packets tx[64g .. 64g + tx_cnt[g])
+    uint32_t tx_base;                // the launch's first packet in the caller's batch (a batch
+                                     // past kMaxLaunch runs as several launches)
     // this batch's slots of the between-batch state (DevState comment) follow from k6 = k % 6
     // (pointers computed where they are used: the kernel's scalar registers are scarce)
     uint32_t k6;
@@ -2039,7 +2041,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerSimd) upe_classify(Args a) {
             const unsigned long long fm = __ballot(live && code == UPE_V_FWD);
             if (live && code == UPE_V_FWD)
                 a.tx[ch * 64u + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = i;
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] =
+                    a.tx_base + i;
             if (lane == 0) a.tx_cnt[ch] = (uint32_t)__popcll(fm);
         }
         // the side array upe_rule_hist reads (lean linear-scan launches never have it; the
@@ -4599,6 +4602,7 @@ namespace {
 // packets (the kernel's per-lane counters are 16-bit halves; a lane sees at most one packet
 // per tile).
 constexpr size_t kMaxLaunch = (size_t)1 << 24;
+static_assert(kMaxLaunch % 64 == 0, "a split launch starts on a 64-packet group (egress list)");
 // A ring launch's completion stamps (upe_gpu_process_ring_emit): batches of `per` packets.
 struct RingReq {
     size_t per;
@@ -4607,7 +4611,7 @@ struct RingReq {
 int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, uint32_t* d_verdict,
                  uint32_t* d_flow_hash, upe_hdr_rec_t* d_hdr, size_t n, void* stream,
                  const RingReq* ring = nullptr, bool host = false, uint32_t* d_tx = nullptr,
-                 uint32_t* d_tx_cnt = nullptr) {
+                 uint32_t* d_tx_cnt = nullptr, size_t tx_base = 0) {
     if (!c) return fail("null context");
     host = host || c->host_tag;
     if (n > 0xFFFFFFFFull - kTile) return fail("batch too large (n must fit in 32 bits)");
@@ -4623,7 +4627,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
             if (process_impl(c, d_frames, d_desc + s0, d_verdict + s0,
                              d_flow_hash ? d_flow_hash + s0 : nullptr, d_hdr ? d_hdr + s0 : nullptr,
                              m, stream, nullptr, host, d_tx ? d_tx + s0 : nullptr,
-                             d_tx_cnt ? d_tx_cnt + s0 / 64 : nullptr) != 0)
+                             d_tx_cnt ? d_tx_cnt + s0 / 64 : nullptr, tx_base + s0) != 0)
                 return -1;
         }
         return 0;
@@ -4657,6 +4661,7 @@ int process_impl(upe_gpu_ctx_t* c, uint8_t* d_frames, const uint64_t* d_desc, ui
     a.n = (uint32_t)n;
     a.tx = d_tx;
     a.tx_cnt = d_tx_cnt;
+    a.tx_base = (uint32_t)tx_base;
     a.rv4 = c->rv4;
     a.rv6 = c->rv6;
     a.fam = c->fam;

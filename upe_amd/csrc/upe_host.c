@@ -385,6 +385,8 @@ int upe_tx_flush_groups(const uint8_t *h_frames, const uint64_t *h_desc, const u
             if (k >= cnt) { g++; k = 0; continue; }
             const uint32_t i = h_tx[g * 64 + k];
             if (i >= end) break; /* the next burst's */
+            if (i < base || count == (int)burst)
+                return host_fail("upe_tx_flush_groups: list entry %d out of packet order%s", (int)i, "");
             frames[count] = h_frames + (h_desc[i] >> 16);
             lens[count++] = (size_t)(h_desc[i] & 0xFFFFu);
             k++;
