@@ -47,6 +47,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <time.h>
+#include <emmintrin.h>
 
 #include "../../include/upe_gpu.h"
 
@@ -102,6 +103,8 @@ typedef struct {
                           rewrites the frames in the pool instead of emitting records */
     int prof;
     uint64_t t_wait, t_walk, t_launch, n_batches, t_flush;
+    uint64_t t_gather, n_empty, n_sleep, n_partial;   /* (profile) gather time, empty pops,
+                                                         idle naps, launches of a partial batch */
     unsigned since_point;  /* batches walked since the last publish with nothing in flight */
 } loop_t;
 
@@ -167,6 +170,25 @@ static void flush_tx(loop_t *L) {
     }
 }
 
+/* A frame's header window into the pinned staging the kernel reads over the link, with
+ * streaming (non-temporal) stores: the lines go to memory without being read for ownership, and
+ * the GPU's read finds them there instead of snooping them out of this core's cache.  (With
+ * cached stores into staging the GPU had just read, the gather cost 57 ns per packet at the
+ * reference's 8192-buffer pool — 2048-packet batches, staging that stays cache-resident — against
+ * 8 ns with 65536-packet batches.)  16-byte pieces; the last one zero-padded past len (the
+ * kernel never reads those bytes).  `win` is 16-byte aligned. */
+static inline void stage_window(uint8_t *win, const uint8_t *d, size_t len) {
+    const size_t c = len < WIN ? len : WIN;
+    size_t o = 0;
+    for (; o + 16 <= c; o += 16)
+        _mm_stream_si128((__m128i *)(win + o), _mm_loadu_si128((const __m128i *)(d + o)));
+    if (o < c) {   /* the last piece: only the frame's own bytes are read */
+        uint8_t t[16] = {0};
+        memcpy(t, d + o, c - o);
+        _mm_stream_si128((__m128i *)(win + o), _mm_loadu_si128((const __m128i *)t));
+    }
+}
+
 /* upe_hdr_apply (upe_host.c) inlined into the walk: one record into its frame. */
 static inline void rec_apply(uint8_t *frame, const upe_hdr_rec_t *rec) {
     const uint8_t fam = rec->b[15];
@@ -193,7 +215,9 @@ static int launch(loop_t *L, int k) {
         rc = upe_gpu_process_mapped(L->ctx, L->pool, S->desc, S->verdict, n, NULL);
     } else {
         /* the header windows in pinned staging, classified where they lie (the kernel reads them
-         * over the link, writes verdicts and records back): one launch, no DMA copies */
+         * over the link, writes verdicts and records back): one launch, no DMA copies; the
+         * streaming stores of the gather drained to memory first */
+        _mm_sfence();
         rc = upe_gpu_process_mapped_emit(L->ctx, S->win, S->desc, S->verdict, S->rec, n, NULL);
     }
     if (rc == 0) rc = upe_gpu_mark(L->ctx, k);
@@ -436,7 +460,9 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
             /* the ring is empty: classify what is gathered now, keeping it in flight while the
              * older batch is walked (a pool too small to fill a batch still overlaps), and walk
              * the last batch in flight once the ring is still empty after that */
+            L.n_empty++;
             if (G->n > 0) {
+                L.n_partial++;
                 if (advance(&L) != 0) goto fail;
                 continue;
             }
@@ -445,6 +471,7 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
                 continue;
             }
             if (ops->stop(user)) break; /* stop signal + ring empty, src/worker.c:270-273 */
+            L.n_sleep++;
             nanosleep(&nap, NULL);
             continue;
         }
@@ -453,6 +480,8 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
         L.bq_len++;
         /* the burst's frames first, their first lines requested together (the producer wrote
          * them on another core: one cross-core transfer each, overlapped) */
+        const uint64_t tg0 = L.prof ? mono_ns() : 0;
+        uint64_t t_adv = 0;   /* (profile) time inside advance() during this burst */
         uint8_t *bd[UPE_TX_BATCH_MAX];
         for (unsigned j = 0; j < k; j++) {
             bd[j] = ops->data(user, burst[j]);
@@ -476,19 +505,24 @@ int upe_gpu_worker_run(upe_gpu_ctx_t *ctx, const upe_worker_ops_t *ops, void *us
                 G->desc[G->n] = UPE_DESC(off, len);
             } else {
                 /* (bytes of the window past len are never read: stale ones may stay) */
-                memcpy(G->win + G->n * WIN, d, len < WIN ? len : WIN);
+                stage_window(G->win + G->n * WIN, d, len);
                 G->desc[G->n] = UPE_DESC(G->n * WIN, len);
             }
             G->data[G->n] = d;
             G->bufs[G->n++] = b;
             G->cut = is_table_write(d, len);
-            if ((G->cut || G->n == L.cap) && advance(&L) != 0) {
-                /* the rest of this burst is held by nobody else: keep it for the drain */
-                G = &L.s[L.g];
-                for (unsigned r = j + 1; r < k; r++) G->bufs[G->n++] = burst[r];
-                goto fail;
+            if (G->cut || G->n == L.cap) {
+                const uint64_t ta = L.prof ? mono_ns() : 0;
+                if (advance(&L) != 0) {
+                    /* the rest of this burst is held by nobody else: keep it for the drain */
+                    G = &L.s[L.g];
+                    for (unsigned r = j + 1; r < k; r++) G->bufs[G->n++] = burst[r];
+                    goto fail;
+                }
+                if (L.prof) t_adv += mono_ns() - ta;
             }
         }
+        if (L.prof) L.t_gather += mono_ns() - tg0 - t_adv;
     }
     goto out;
 fail:
@@ -497,11 +531,14 @@ fail:
 out:
     if (L.prof)
         fprintf(stderr, "upe_worker: %.3f s total, %llu batches (%.0f packets each): launch %.3f s, "
-                "GPU wait %.3f s, walk %.3f s (of which TX flushes %.3f s), rest (pop + gather + idle) %.3f s\n",
+                "GPU wait %.3f s, walk %.3f s (of which TX flushes %.3f s), rest (pop + gather + idle) %.3f s "
+                "(gather %.3f s; empty pops %llu, partial launches %llu, naps %llu)\n",
                 (mono_ns() - t_start) * 1e-9, (unsigned long long)L.n_batches,
                 L.n_batches ? (double)L.c.pkts_in / (double)L.n_batches : 0.0, L.t_launch * 1e-9,
                 L.t_wait * 1e-9, L.t_walk * 1e-9, L.t_flush * 1e-9,
-                (mono_ns() - t_start - L.t_launch - L.t_wait - L.t_walk) * 1e-9);
+                (mono_ns() - t_start - L.t_launch - L.t_wait - L.t_walk) * 1e-9, L.t_gather * 1e-9,
+                (unsigned long long)L.n_empty, (unsigned long long)L.n_partial,
+                (unsigned long long)L.n_sleep);
     if (counters) *counters = L.c;
     (void)upe_gpu_tag_host(ctx, 0);
     free(L.bq);
